@@ -1,0 +1,460 @@
+// BatchNorm bookkeeping, decoder output (BN + Sigmoid + reconstruction loss) and the decoder
+// Linear -> BatchNorm1d backward for gfx950.
+//
+// Reference arithmetic replaced:
+//   nn.BatchNorm2d/1d running statistics (momentum 0.1, unbiased running var)   vae.py:17-44
+//   decoder tail BatchNorm2d(C) + Sigmoid                                       vae.py:44-45, 154-155
+//   vae_loss reconstruction term: mean_n sum_{chw} (xhat - x)^2                 losses.py:36-47
+//   decoder Linear(z, 2048) -> BatchNorm1d(2048) -> ReLU backward               vae.py:33-35
+#include "cv_common.hpp"
+
+namespace cv {
+
+// ---------------------------------------------------------------- running statistics
+constexpr int MAX_BN = 16;
+struct RunArgs {
+  cv_bn bn[MAX_BN];
+  int64_t* nbt[MAX_BN];
+  int nl;
+  float momentum;
+};
+
+__global__ __launch_bounds__(256) void bn_running_kernel(const RunArgs a) {
+  const int l = blockIdx.y;
+  if (l >= a.nl) return;
+  const cv_bn& b = a.bn[l];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c == 0 && a.nbt[l]) a.nbt[l][0] += 1;
+  if (c >= b.C) return;
+  double s = 0.0, q = 0.0;
+#pragma unroll
+  for (int r = 0; r < CV_STAT_REPL; ++r) {
+    s += b.stat[(size_t)r * 2 * b.C + c];
+    q += b.stat[(size_t)r * 2 * b.C + b.C + c];
+  }
+  const double n = (double)b.count;
+  const double mean = s / n;
+  double var = q / n - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double unbiased = (b.count > 1) ? var * n / (n - 1.0) : var;
+  float* rm = const_cast<float*>(b.running_mean);
+  float* rv = const_cast<float*>(b.running_var);
+  const float m = a.momentum;
+  rm[c] = m * (float)mean + (1.0f - m) * rm[c];
+  rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
+}
+
+struct GradArgs {
+  cv_bn bn[MAX_BN];
+  float* dg[MAX_BN];
+  float* db[MAX_BN];
+  int nl;
+};
+__global__ __launch_bounds__(256) void bn_grads_kernel(const GradArgs a) {
+  const int l = blockIdx.y;
+  if (l >= a.nl) return;
+  const cv_bn& b = a.bn[l];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= b.C) return;
+  double s = 0.0, q = 0.0;
+#pragma unroll
+  for (int r = 0; r < CV_STAT_REPL; ++r) {
+    s += b.gstat[(size_t)r * 2 * b.C + c];
+    q += b.gstat[(size_t)r * 2 * b.C + b.C + c];
+  }
+  if (a.db[l]) a.db[l][c] = (float)s;
+  if (a.dg[l]) a.dg[l][c] = (float)q;
+}
+
+__global__ void bn_stats_kernel(const cv_bn b, float* mean, float* invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= b.C) return;
+  float m, is;
+  bn_mean_istd(b, c, m, is);
+  mean[c] = m;
+  invstd[c] = is;
+}
+
+// ---------------------------------------------------------------- decoder output
+// xhat (NCHW) = sigmoid((y - mu)*sc + beta), y NHWC.  One thread per output element in NCHW order.
+constexpr int OUT_MAXC = 4;
+
+__global__ __launch_bounds__(256) void output_fwd_kernel(const cv_bn b, const float* __restrict__ y, int n, int c,
+                                                         int hw, float* __restrict__ xhat) {
+  __shared__ BnFwdC k[OUT_MAXC];
+  if (threadIdx.x < c) k[threadIdx.x] = bn_fwd_const(b, threadIdx.x);
+  __syncthreads();
+  const long total = (long)n * c * hw;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int p = (int)(i % hw);
+    const long nc = i / hw;
+    const int ch = (int)(nc % c);
+    const long img = nc / c;
+    const float v = bn_out(y[(img * hw + p) * c + ch], k[ch]);
+    xhat[i] = 1.0f / (1.0f + expf(-v));
+  }
+}
+
+// Fused output + reconstruction loss + backward seed.  Elements are visited in NHWC order so the
+// dv store (NHWC) is coalesced; x / xhat are NCHW.
+__global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const float* __restrict__ y,
+                                                          const float* __restrict__ x, int n, int c, int hw,
+                                                          float* __restrict__ xhat, double* rec_out,
+                                                          float* __restrict__ dv, double* gstat,
+                                                          const float* rec_scale) {
+  __shared__ BnFwdC k[OUT_MAXC];
+  __shared__ float2 mi[OUT_MAXC];
+  __shared__ double red[4][1 + 2 * OUT_MAXC];
+  if (threadIdx.x < c) {
+    k[threadIdx.x] = bn_fwd_const(b, threadIdx.x);
+    float m_, i_;
+    bn_mean_istd(b, threadIdx.x, m_, i_);
+    mi[threadIdx.x] = make_float2(m_, i_);
+  }
+  __syncthreads();
+  const float scale = (rec_scale ? rec_scale[0] : 1.0f) * 2.0f / (float)n;
+  const long total = (long)n * c * hw;
+  float rec = 0.f;
+  float s1[OUT_MAXC], s2[OUT_MAXC];
+#pragma unroll
+  for (int j = 0; j < OUT_MAXC; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int ch = (int)(i % c);
+    const long pix = i / c;  // img*hw + p
+    const long img = pix / hw;
+    const int p = (int)(pix - img * hw);
+    const long nchw = (img * c + ch) * hw + p;
+    const float yv = y[i];
+    const float v = bn_out(yv, k[ch]);
+    const float xh = 1.0f / (1.0f + expf(-v));
+    const float diff = xh - x[nchw];
+    xhat[nchw] = xh;
+    rec = fmaf(diff, diff, rec);
+    if (dv) {
+      const float d = scale * diff * xh * (1.0f - xh);
+      dv[i] = d;
+#pragma unroll
+      for (int j = 0; j < OUT_MAXC; ++j)
+        if (j == ch) {
+          s1[j] += d;
+          s2[j] += d * ((yv - mi[ch].x) * mi[ch].y);
+        }
+    }
+  }
+  // block reduction (fp64 for the outputs)
+  double vals[1 + 2 * OUT_MAXC];
+  vals[0] = (double)rec;
+#pragma unroll
+  for (int j = 0; j < OUT_MAXC; ++j) { vals[1 + j] = (double)s1[j]; vals[1 + OUT_MAXC + j] = (double)s2[j]; }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 1 + 2 * OUT_MAXC; ++q) {
+    double v = wave_sum(vals[q]);
+    if (lane == 0) red[w][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    atomic_add_f64(rec_out, r / (double)n);
+    if (dv) {
+      const int repl = blockIdx.x % CV_STAT_REPL;
+      for (int j = 0; j < c; ++j) {
+        const double a = red[0][1 + j] + red[1][1 + j] + red[2][1 + j] + red[3][1 + j];
+        const double bb = red[0][1 + OUT_MAXC + j] + red[1][1 + OUT_MAXC + j] + red[2][1 + OUT_MAXC + j] +
+                          red[3][1 + OUT_MAXC + j];
+        atomic_add_f64(gstat + (size_t)repl * 2 * c + j, a);
+        atomic_add_f64(gstat + (size_t)repl * 2 * c + c + j, bb);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void output_bwd_kernel(const cv_bn b, const float* __restrict__ y,
+                                                         const float* __restrict__ xhat,
+                                                         const float* __restrict__ dxhat, int n, int c, int hw,
+                                                         float* __restrict__ dv, double* gstat) {
+  __shared__ float2 mi[OUT_MAXC];
+  __shared__ double red[4][2 * OUT_MAXC];
+  if (threadIdx.x < c) {
+    float m_, i_;
+    bn_mean_istd(b, threadIdx.x, m_, i_);
+    mi[threadIdx.x] = make_float2(m_, i_);
+  }
+  __syncthreads();
+  const long total = (long)n * c * hw;
+  float s1[OUT_MAXC], s2[OUT_MAXC];
+#pragma unroll
+  for (int j = 0; j < OUT_MAXC; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int ch = (int)(i % c);
+    const long pix = i / c;
+    const long img = pix / hw;
+    const int p = (int)(pix - img * hw);
+    const long nchw = (img * c + ch) * hw + p;
+    const float xh = xhat[nchw];
+    const float d = dxhat[nchw] * xh * (1.0f - xh);
+    dv[i] = d;
+#pragma unroll
+    for (int j = 0; j < OUT_MAXC; ++j)
+      if (j == ch) {
+        s1[j] += d;
+        s2[j] += d * ((y[i] - mi[ch].x) * mi[ch].y);
+      }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < OUT_MAXC; ++j) {
+    double a = wave_sum((double)s1[j]), bb = wave_sum((double)s2[j]);
+    if (lane == 0) { red[w][j] = a; red[w][OUT_MAXC + j] = bb; }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int repl = blockIdx.x % CV_STAT_REPL;
+    for (int j = 0; j < c; ++j) {
+      atomic_add_f64(gstat + (size_t)repl * 2 * c + j, red[0][j] + red[1][j] + red[2][j] + red[3][j]);
+      atomic_add_f64(gstat + (size_t)repl * 2 * c + c + j,
+                     red[0][OUT_MAXC + j] + red[1][OUT_MAXC + j] + red[2][OUT_MAXC + j] + red[3][OUT_MAXC + j]);
+    }
+  }
+}
+
+// BN1d(+ReLU) applied elementwise; the tensor is stored in the Unflatten/NHWC order.  Thread =
+// one storage column (constants computed once), looping over a chunk of rows: coalesced rows.
+constexpr int BA_ROWS = 8;
+__global__ __launch_bounds__(256) void bn_apply_kernel(const cv_bn b, const float* __restrict__ x,
+                                                       float* __restrict__ out, int rows, int F, int pix, int ch,
+                                                       int relu) {
+  const int col = blockIdx.x * 256 + threadIdx.x;  // storage position p*ch + c
+  if (col >= F) return;
+  const int f = (pix > 1) ? (col % ch) * pix + col / ch : col;  // PyTorch feature c*pix + p
+  const BnFwdC k = bn_fwd_const(b, f);
+  const int r0 = blockIdx.y * BA_ROWS;
+  for (int r = r0; r < min(rows, r0 + BA_ROWS); ++r) {
+    const size_t i = (size_t)r * F + col;
+    const float v = bn_out(x[i], k);
+    out[i] = relu ? fmaxf(v, 0.f) : v;
+  }
+}
+
+static int elem_grid(long total) {
+  long g = (total + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// ---------------------------------------------------------------- decoder Linear -> BN1d backward
+// Block = 64 features (PyTorch order f); phase 1 masks da in place and reduces the BN1d backward
+// sums over the whole batch; phase 2 forms dW[f][k] = sum_n BNbwd(dz)[n][f] * z[n][k].
+constexpr int DL_F = 64;
+constexpr int DL_NCH = 64;   // batch rows per LDS chunk
+constexpr int DL_KMAX = 128; // latent width limit
+
+__global__ __launch_bounds__(256) void declinear_bwd_kernel(int n, int F, int K, int pix, int ch, float* da,
+                                                            const float* __restrict__ h, const cv_bn b, double* gstat,
+                                                            const float* __restrict__ z, float* __restrict__ gw) {
+  __shared__ float sd[DL_NCH][DL_F + 1];
+  __shared__ float sz[DL_NCH][DL_KMAX + 1];
+  __shared__ float r1[4][DL_F], r2[4][DL_F];
+  __shared__ BnFwdC kf[DL_F];
+  __shared__ BnBwdC kb[DL_F];
+  const int t = threadIdx.x;
+  const int f0 = blockIdx.x * DL_F;
+  if (t < DL_F && f0 + t < F) {
+    kf[t] = bn_fwd_const(b, f0 + t);
+    float m_, i_;
+    bn_mean_istd(b, f0 + t, m_, i_);
+    kb[t].mu = m_;
+    kb[t].istd = i_;
+    kb[t].sc = kf[t].sc;
+  }
+  __syncthreads();
+  // phase 1
+  {
+    const int fl = t % DL_F, rg = t / DL_F;
+    const int f = f0 + fl;
+    float s1 = 0.f, s2 = 0.f;
+    if (f < F) {
+      const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
+      for (int r = rg; r < n; r += 4) {
+        const size_t off = (size_t)r * F + col;
+        const float hv = h[off];
+        float d = da[off];
+        if (bn_out(hv, kf[fl]) <= 0.f) d = 0.f;
+        da[off] = d;
+        s1 += d;
+        s2 += d * ((hv - kb[fl].mu) * kb[fl].istd);
+      }
+    }
+    r1[rg][fl] = s1;
+    r2[rg][fl] = s2;
+  }
+  __syncthreads();
+  if (t < DL_F && f0 + t < F) {
+    const double a = (double)r1[0][t] + r1[1][t] + r1[2][t] + r1[3][t];
+    const double q = (double)r2[0][t] + r2[1][t] + r2[2][t] + r2[3][t];
+    gstat[f0 + t] = a;
+    gstat[F + f0 + t] = q;
+    kb[t].c1 = (float)(a / (double)b.count);
+    kb[t].c2 = (float)(q / (double)b.count);
+  }
+  __syncthreads();
+  // phase 2: each thread owns outputs (f = f0 + t % 64, k = t / 64 + 4j)
+  const int fl = t % DL_F, kg = t / DL_F;
+  constexpr int KPT = DL_KMAX / 4;
+  float acc[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) acc[j] = 0.f;
+  for (int r0 = 0; r0 < n; r0 += DL_NCH) {
+    __syncthreads();
+    // stage BN-backward dz for 64 rows x 64 features
+    for (int e = t; e < DL_NCH * DL_F; e += 256) {
+      const int rr = e / DL_F, ff = e % DL_F;
+      const int r = r0 + rr, f = f0 + ff;
+      float v = 0.f;
+      if (r < n && f < F) {
+        const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
+        const size_t off = (size_t)r * F + col;
+        v = bn_bwd(da[off], h[off], kb[ff]);
+      }
+      sd[rr][ff] = v;
+    }
+    for (int e = t; e < DL_NCH * K; e += 256) {
+      const int rr = e / K, kk = e % K;
+      const int r = r0 + rr;
+      sz[rr][kk] = (r < n) ? z[(size_t)r * K + kk] : 0.f;
+    }
+    __syncthreads();
+    const int rmax = min(DL_NCH, n - r0);
+    for (int rr = 0; rr < rmax; ++rr) {
+      const float dv = sd[rr][fl];
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const int kk = kg + 4 * j;
+        if (kk < K) acc[j] = fmaf(dv, sz[rr][kk], acc[j]);
+      }
+    }
+  }
+  if (f0 + fl < F) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int kk = kg + 4 * j;
+      if (kk < K) gw[(size_t)(f0 + fl) * K + kk] = acc[j];
+    }
+  }
+}
+
+}  // namespace cv
+
+using namespace cv;
+
+extern "C" int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum, int64_t* const* nbt,
+                                    cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && nlayers > 0 && nlayers <= MAX_BN, "bn_update_running: 1..%d layers", MAX_BN);
+  RunArgs a;
+  memset(&a, 0, sizeof(a));
+  int cmax = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    CV_REQUIRE(bn[i].stat && bn[i].running_mean && bn[i].running_var && bn[i].C > 0 && bn[i].count > 0,
+               "bn_update_running: layer %d incomplete", i);
+    a.bn[i] = bn[i];
+    a.nbt[i] = nbt ? nbt[i] : nullptr;
+    cmax = bn[i].C > cmax ? bn[i].C : cmax;
+  }
+  a.nl = nlayers;
+  a.momentum = momentum;
+  hipLaunchKernelGGL(bn_running_kernel, dim3(cdiv(cmax, 256), nlayers), dim3(256), 0, S(stream), a);
+  CV_LAUNCH_CHECK("bn_update_running");
+  return 0;
+}
+
+extern "C" int cv_bn_apply(const cv_bn* bn, const float* x, float* out, int rows, int features, int pix, int ch,
+                           int relu, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && x && out && rows > 0 && features > 0 && bn->C == features, "bn_apply: bad args");
+  CV_REQUIRE(pix <= 1 || pix * ch == features, "bn_apply: pix*ch != features");
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(cdiv(features, 256), cdiv(rows, BA_ROWS)), dim3(256), 0, S(stream), *bn,
+                     x, out, rows, features, pix, ch, relu);
+  CV_LAUNCH_CHECK("bn_apply");
+  return 0;
+}
+
+extern "C" int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dgamma, float* const* dbeta,
+                                 cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && nlayers > 0 && nlayers <= MAX_BN && dgamma && dbeta, "bn_param_grads: 1..%d layers", MAX_BN);
+  GradArgs a;
+  memset(&a, 0, sizeof(a));
+  int cmax = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    CV_REQUIRE(bn[i].gstat && bn[i].C > 0, "bn_param_grads: layer %d incomplete", i);
+    a.bn[i] = bn[i];
+    a.dg[i] = dgamma[i];
+    a.db[i] = dbeta[i];
+    cmax = bn[i].C > cmax ? bn[i].C : cmax;
+  }
+  a.nl = nlayers;
+  hipLaunchKernelGGL(bn_grads_kernel, dim3(cdiv(cmax, 256), nlayers), dim3(256), 0, S(stream), a);
+  CV_LAUNCH_CHECK("bn_param_grads");
+  return 0;
+}
+
+extern "C" int cv_bn_batch_stats(const cv_bn* bn, float* mean, float* invstd, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && mean && invstd && bn->C > 0, "bn_batch_stats: bad args");
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(cdiv(bn->C, 256)), dim3(256), 0, S(stream), *bn, mean, invstd);
+  CV_LAUNCH_CHECK("bn_batch_stats");
+  return 0;
+}
+
+extern "C" int cv_output_forward(const cv_bn* bn, const float* y, int n, int c, int hw, float* xhat,
+                                 cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && y && xhat && n > 0 && c > 0 && c <= OUT_MAXC && hw > 0, "output_forward: bad args (C<=%d)",
+             OUT_MAXC);
+  CV_REQUIRE(bn->C == c, "output_forward: BN width %d != %d", bn->C, c);
+  hipLaunchKernelGGL(output_fwd_kernel, dim3(elem_grid((long)n * c * hw)), dim3(256), 0, S(stream), *bn, y, n, c, hw,
+                     xhat);
+  CV_LAUNCH_CHECK("output_forward");
+  return 0;
+}
+
+extern "C" int cv_output_loss(const cv_bn* bn, const float* y, const float* x, int n, int c, int hw, float* xhat,
+                              double* rec_out, float* dv_out, double* gstat_out, const float* rec_scale,
+                              cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && y && x && xhat && rec_out && n > 0 && c > 0 && c <= OUT_MAXC && hw > 0,
+             "output_loss: bad args (C<=%d)", OUT_MAXC);
+  CV_REQUIRE(bn->C == c, "output_loss: BN width %d != %d", bn->C, c);
+  CV_REQUIRE(!dv_out || gstat_out, "output_loss: dv needs gstat_out");
+  hipLaunchKernelGGL(output_loss_kernel, dim3(elem_grid((long)n * c * hw)), dim3(256), 0, S(stream), *bn, y, x, n, c,
+                     hw, xhat, rec_out, dv_out, gstat_out, rec_scale);
+  CV_LAUNCH_CHECK("output_loss");
+  return 0;
+}
+
+extern "C" int cv_output_backward(const cv_bn* bn, const float* y, const float* xhat, const float* dxhat, int n,
+                                  int c, int hw, float* dv_out, double* gstat_out, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && y && xhat && dxhat && dv_out && gstat_out && n > 0 && c > 0 && c <= OUT_MAXC && hw > 0,
+             "output_backward: bad args");
+  hipLaunchKernelGGL(output_bwd_kernel, dim3(elem_grid((long)n * c * hw)), dim3(256), 0, S(stream), *bn, y, xhat,
+                     dxhat, n, c, hw, dv_out, gstat_out);
+  CV_LAUNCH_CHECK("output_backward");
+  return 0;
+}
+
+extern "C" int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, const cv_bn* bn,
+                                            double* gstat_out, const float* zin, float* gweight, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(g && da && h && bn && gstat_out && zin && gweight, "declinear_backward_weight: null args");
+  CV_REQUIRE(g->in_features <= DL_KMAX, "declinear_backward_weight: latent width %d > %d", g->in_features,
+             DL_KMAX);
+  CV_REQUIRE(bn->C == g->out_features && bn->train, "declinear_backward_weight: BN1d must be train-mode, C=out");
+  const int pix = g->out_pix > 0 ? g->out_pix : 1;
+  hipLaunchKernelGGL(declinear_bwd_kernel, dim3(cdiv(g->out_features, DL_F)), dim3(256), 0, S(stream), g->n,
+                     g->out_features, g->in_features, pix, g->out_ch, da, h, *bn, gstat_out, zin, gweight);
+  CV_LAUNCH_CHECK("declinear_backward_weight");
+  return 0;
+}

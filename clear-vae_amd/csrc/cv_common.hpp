@@ -1,0 +1,173 @@
+// Shared device/host helpers for libclearvae_hip.so (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <string.h>
+#include "../../include/clearvae.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace cv {
+
+// ---------------------------------------------------------------- host error plumbing
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define CV_REQUIRE(cond, ...)                \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::cv::set_error(__VA_ARGS__);          \
+      return 1;                              \
+    }                                        \
+  } while (0)
+
+#define CV_LAUNCH_CHECK(name)                                                   \
+  do {                                                                          \
+    hipError_t e_ = hipGetLastError();                                          \
+    if (e_ != hipSuccess) {                                                     \
+      ::cv::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));    \
+      return 2;                                                                 \
+    }                                                                           \
+  } while (0)
+
+static inline hipStream_t S(cv_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------- wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x == NT (multiple of 64); scratch >= NT/64 entries; result in all threads
+template <int NT, class T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  T r = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += scratch[i];
+  return r;
+}
+
+// ---------------------------------------------------------------- BatchNorm constants
+// Per-feature constants derived from the fp64 replica sums (or running stats in eval mode).
+struct BnFwdC { float sc, mu, be, istd; };      // a = max((x - mu)*sc + be, 0), sc = gamma*istd
+struct BnBwdC { float sc, mu, istd, c1, c2; };   // dy = sc*(dz - c1 - (y-mu)*istd*c2)
+
+__device__ __forceinline__ void bn_mean_istd(const cv_bn& b, int c, float& mean, float& istd) {
+  if (b.train) {
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int r = 0; r < CV_STAT_REPL; ++r) {
+      s += b.stat[(size_t)r * 2 * b.C + c];
+      q += b.stat[(size_t)r * 2 * b.C + b.C + c];
+    }
+    const double inv_n = 1.0 / (double)b.count;
+    const double m = s * inv_n;
+    double var = q * inv_n - m * m;
+    if (var < 0.0) var = 0.0;
+    mean = (float)m;
+    istd = (float)(1.0 / sqrt(var + (double)b.eps));
+  } else {
+    mean = b.running_mean[c];
+    istd = (float)(1.0 / sqrt((double)b.running_var[c] + (double)b.eps));
+  }
+}
+
+__device__ __forceinline__ BnFwdC bn_fwd_const(const cv_bn& b, int c) {
+  float mean, istd;
+  bn_mean_istd(b, c, mean, istd);
+  const float g = b.gamma ? b.gamma[c] : 1.f, be = b.beta ? b.beta[c] : 0.f;
+  BnFwdC r;
+  r.sc = g * istd;
+  r.mu = mean;
+  r.be = be;
+  r.istd = istd;
+  return r;
+}
+
+__device__ __forceinline__ BnBwdC bn_bwd_const(const cv_bn& b, int c) {
+  float mean, istd;
+  bn_mean_istd(b, c, mean, istd);
+  const float g = b.gamma ? b.gamma[c] : 1.f;
+  BnBwdC r;
+  r.sc = g * istd;
+  r.mu = mean;
+  r.istd = istd;
+  if (b.train) {
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < CV_STAT_REPL; ++rr) {
+      s += b.gstat[(size_t)rr * 2 * b.C + c];
+      q += b.gstat[(size_t)rr * 2 * b.C + b.C + c];
+    }
+    r.c1 = (float)(s / (double)b.count);
+    r.c2 = (float)(q / (double)b.count);
+  } else {
+    r.c1 = 0.f;
+    r.c2 = 0.f;
+  }
+  return r;
+}
+
+// (x - mu) first: the subtraction is exact for x near mu, so the sign test of a near-zero BN output
+// (the ReLU mask) agrees with an fp64 evaluation far more often than x*sc + (beta - mu*sc) does.
+__device__ __forceinline__ float bn_out(float x, BnFwdC k) { return fmaf(x - k.mu, k.sc, k.be); }
+__device__ __forceinline__ float bn_relu(float x, BnFwdC k) { return fmaxf(bn_out(x, k), 0.f); }
+__device__ __forceinline__ float bn_bwd(float dz, float y, BnBwdC k) {
+  return k.sc * (dz - k.c1 - (y - k.mu) * k.istd * k.c2);
+}
+
+__device__ __forceinline__ void atomic_add_f64(double* p, double v) { atomicAdd(p, v); }
+
+// ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
+struct u32x4 { uint32_t x, y, z, w; };
+__device__ __forceinline__ u32x4 philox(uint64_t key, uint64_t ctr_hi, uint64_t ctr_lo) {
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+  uint32_t c0 = (uint32_t)ctr_lo, c1 = (uint32_t)(ctr_lo >> 32);
+  uint32_t c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+__device__ __forceinline__ float u01(uint32_t v) {  // (0,1]
+  return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+// two standard normals from one Philox draw
+__device__ __forceinline__ void normal2(uint64_t seed, uint64_t offset, uint64_t idx, float& a, float& b) {
+  const u32x4 r = philox(seed, offset, idx);
+  const float u1 = u01(r.x), u2 = u01(r.y);
+  const float rad = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  sincosf(6.283185307179586f * u2, &s, &c);
+  a = rad * c;
+  b = rad * s;
+}
+
+}  // namespace cv

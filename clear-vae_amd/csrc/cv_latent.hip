@@ -1,0 +1,601 @@
+// Latent-space kernels of the CLEAR-VAE step on gfx950:
+//   reparameterisation (vae.py:56-79), KL + reparam chain rule (losses.py:48-49), the
+//   reconstruction MSE of the autograd path (losses.py:45-47), and the SNN / NT-Xent contrastive
+//   loss with its five similarity measures (losses.py:53-137) in two row-parallel passes:
+//     rows : online log-sum-exp of S_ij/tau over all j and over positive pairs (one wave per row)
+//     grad : dtheta_i = sum_j (G_ij + G_ji) dS_ij/dtheta_i with G = (q - p)/(nf*tau) on finite rows
+//   (S is exactly symmetric for every measure, so only the row derivative is needed).
+#include "cv_common.hpp"
+
+namespace cv {
+
+// ---------------------------------------------------------------- reparameterisation
+// One workgroup; offset[0] is read by every thread and advanced by thread 0 after a barrier.
+__global__ __launch_bounds__(1024) void reparam_kernel(const float* __restrict__ heads, int n, int d,
+                                                       const float* __restrict__ eps_in, uint64_t seed,
+                                                       uint64_t* offset, float* __restrict__ z,
+                                                       float* __restrict__ eps_out) {
+  const uint64_t off = offset ? offset[0] : 0;
+  const int zd = 2 * d;
+  const long total = (long)n * zd;
+  for (long p = threadIdx.x; 2 * p < total; p += blockDim.x) {
+    float e2[2];
+    if (!eps_in) normal2(seed, off, (uint64_t)p, e2[0], e2[1]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const long e = 2 * p + q;
+      if (e >= total) break;
+      const int row = (int)(e / zd), j = (int)(e % zd);
+      const int blk = (j < d) ? 0 : 2;  // c: mu at 0, lv at d ; s: mu at 2d, lv at 3d
+      const int k = (j < d) ? j : j - d;
+      const float mu = heads[(size_t)row * 4 * d + blk * d + k];
+      const float lv = heads[(size_t)row * 4 * d + (blk + 1) * d + k];
+      const float ep = eps_in ? eps_in[e] : e2[q];
+      const float sd = expf(0.5f * lv);
+      z[e] = mu + ep * sd;
+      if (eps_out) eps_out[e] = ep;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && offset) offset[0] = off + 1;
+}
+
+// single factor (module path): z = mu + eps*exp(lv/2); grid-stride, offset advanced by the last block
+__global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
+                                                     long numel, const float* __restrict__ eps_in, uint64_t seed,
+                                                     uint64_t* offset, float* __restrict__ z) {
+  const uint64_t off = offset ? offset[0] : 0;
+  for (long p = (long)blockIdx.x * 256 + threadIdx.x; 2 * p < numel; p += (long)gridDim.x * 256) {
+    float e2[2];
+    if (!eps_in) normal2(seed, off, (uint64_t)p, e2[0], e2[1]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const long e = 2 * p + q;
+      if (e >= numel) break;
+      const float ep = eps_in ? eps_in[e] : e2[q];
+      z[e] = mu[e] + ep * expf(0.5f * lv[e]);
+    }
+  }
+  if (offset) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long prev = atomicAdd((unsigned long long*)(offset + 1), 1ull);
+      if (prev == (unsigned long long)(gridDim.x - 1)) {
+        offset[0] = off + 1;
+        offset[1] = 0;
+      }
+    }
+  }
+}
+__global__ __launch_bounds__(256) void sample_bwd_kernel(const float* __restrict__ mu, const float* __restrict__ z,
+                                                         const float* __restrict__ dz, long numel, float* dmu,
+                                                         float* dlv, int accumulate) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < numel; e += (long)gridDim.x * 256) {
+    const float g = dz[e];
+    const float gl = g * (z[e] - mu[e]) * 0.5f;
+    dmu[e] = accumulate ? dmu[e] + g : g;
+    dlv[e] = accumulate ? dlv[e] + gl : gl;
+  }
+}
+
+// ---------------------------------------------------------------- KL (+ combination with dz)
+// kl = -0.5/n * sum(1 + lv - mu^2 - exp(lv)); d kl/d mu = mu/n, d kl/d lv = -0.5/n (1 - exp(lv)).
+// Deterministic: one workgroup, fixed-order tree reduction.
+__global__ __launch_bounds__(1024) void kl_kernel(const float* __restrict__ mu, const float* __restrict__ lv, int ld,
+                                                  int n, int d, float* kl_out, const float* gscale,
+                                                  float* dmu, float* dlv, int gld, int accumulate) {
+  __shared__ double scratch[16];
+  double s = 0.0;
+  const float g = gscale ? gscale[0] : 1.0f;
+  const float inv_n = 1.0f / (float)n;
+  for (int e = threadIdx.x; e < n * d; e += blockDim.x) {
+    const int r = e / d, k = e % d;
+    const float m = mu[(size_t)r * ld + k], l = lv[(size_t)r * ld + k];
+    const float el = expf(l);
+    s += (double)(1.0f + l - m * m - el);
+    if (dmu) {
+      const float gm = g * m * inv_n;
+      const float gl = g * (-0.5f * inv_n) * (1.0f - el);
+      float* pm = dmu + (size_t)r * gld + k;
+      float* pl = dlv + (size_t)r * gld + k;
+      *pm = accumulate ? *pm + gm : gm;
+      *pl = accumulate ? *pl + gl : gl;
+    }
+  }
+  const double tot = block_sum<1024>(s, scratch);
+  if (threadIdx.x == 0 && kl_out) kl_out[0] = (float)(-0.5 * tot / (double)n);
+}
+
+// Fused step version: dheads = [dmu_c, dlv_c, dmu_s, dlv_s] from KL (weight w from the annealer) and
+// the decoder gradient dz through z = mu + eps*exp(lv/2).  losses[1..2] = kl_c, kl_s; losses[7] = w.
+__global__ __launch_bounds__(1024) void combine_kernel(const float* __restrict__ heads, const float* __restrict__ z,
+                                                       const float* __restrict__ dz, int n, int d, float beta,
+                                                       float loc, float scale, const int64_t* anneal_step,
+                                                       const double* rec_in, float* __restrict__ dheads,
+                                                       float* losses) {
+  __shared__ double scratch[16];
+  const double t = (double)anneal_step[0];
+  // LogisticAnnealer.slope (trainer.py:32-34): beta / (1 + exp(-(t - loc)/scale)), in double
+  const float w = (float)((double)beta / (1.0 + exp(-(t - (double)loc) / (double)scale)));
+  const float inv_n = 1.0f / (float)n;
+  double sc = 0.0, ss = 0.0;
+  const int zd = 2 * d;
+  for (int e = threadIdx.x; e < n * zd; e += blockDim.x) {
+    const int r = e / zd, j = e % zd;
+    const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
+    const float m = heads[(size_t)r * 4 * d + blk * d + k];
+    const float l = heads[(size_t)r * 4 * d + (blk + 1) * d + k];
+    const float el = expf(l);
+    const double term = (double)(1.0f + l - m * m - el);
+    if (j < d) sc += term; else ss += term;
+    const float g = dz ? dz[e] : 0.f;
+    const float zz = z[e];
+    dheads[(size_t)r * 4 * d + blk * d + k] = w * m * inv_n + g;
+    dheads[(size_t)r * 4 * d + (blk + 1) * d + k] = w * (-0.5f * inv_n) * (1.0f - el) + g * (zz - m) * 0.5f;
+  }
+  const double kc = block_sum<1024>(sc, scratch);
+  const double ks = block_sum<1024>(ss, scratch);
+  if (threadIdx.x == 0) {
+    if (rec_in) losses[0] = (float)rec_in[0];
+    losses[1] = (float)(-0.5 * kc / (double)n);
+    losses[2] = (float)(-0.5 * ks / (double)n);
+    losses[7] = w;
+  }
+}
+
+// ---------------------------------------------------------------- reconstruction MSE (autograd path)
+__global__ __launch_bounds__(1024) void mse_kernel(const float* __restrict__ xh, const float* __restrict__ x, long total,
+                                                   int n, float* rec_out, double* acc) {
+  // multi-block: partial sums to acc (fp64 atomics); last block writes rec_out
+  __shared__ double scratch[16];
+  double s = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const float dd = xh[i] - x[i];
+    s += (double)(dd * dd);
+  }
+  s = block_sum<1024>(s, scratch);
+  if (threadIdx.x == 0) atomic_add_f64(acc, s);
+}
+__global__ void mse_finish_kernel(const double* acc, int n, float* rec_out) {
+  if (threadIdx.x == 0) rec_out[0] = (float)(acc[0] / (double)n);
+}
+__global__ __launch_bounds__(256) void mse_bwd_kernel(const float* __restrict__ xh, const float* __restrict__ x,
+                                                      long total, int n, const float* gscale, float* dxh) {
+  const float g = (gscale ? gscale[0] : 1.0f) * 2.0f / (float)n;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+    dxh[i] = g * (xh[i] - x[i]);
+}
+
+// ---------------------------------------------------------------- NT-Xent
+struct Branch {
+  const float* mu;
+  const float* lv;
+  int ld;
+  int ps;
+  float* dmu;
+  float* dlv;
+  int gld;
+  const float* gscale;
+  float gmul;
+  float* loss_out;
+  float* lse;  // [2n]: lse_all, lse_pos (units of S/tau)
+};
+constexpr int MAXBR = 2;
+struct NtArgs {
+  Branch br[MAXBR];
+  const int64_t* label;
+  int n, d, sim;
+  float tau;
+  int accumulate;
+};
+
+constexpr int NT_ROWS = 4;   // rows (waves) per 256-thread block
+constexpr int NT_MAXN = 4096;
+
+// similarity of row i (theta_i) and column j
+template <int DM>
+__device__ __forceinline__ float sim_ij(int sim, const float* mi, const float* li, float ni, const float* mj,
+                                        const float* lj, float nj, int d) {
+  float s = 0.f;
+  if (sim == CV_SIM_COSINE) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) s += (mj[k] / nj) * (mi[k] / ni);
+    return s;
+  }
+  if (sim == CV_SIM_L2) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) {
+        const float df = mj[k] - mi[k];
+        s += df * df;
+      }
+    return -s;
+  }
+  if (sim == CV_SIM_MODIFIED_L2) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) {
+        const float df = mj[k] - mi[k];
+        s += df * df / expf(0.5f * (lj[k] + li[k]));
+      }
+    return -s;
+  }
+  if (sim == CV_SIM_MAHALANOBIS) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) {
+        const float df = mj[k] - mi[k];
+        s += df * df / (0.5f * (expf(lj[k]) + expf(li[k])));
+      }
+    return -s;
+  }
+  // jeffrey: kl[i,j] = 0.5(L_j - L_i - d + sum D/v_j + sum v_j/(v_i + 1e-8)); S = -0.5(kl_ij + kl_ji)
+  float Li = 0.f, Lj = 0.f, t2ij = 0.f, t3ij = 0.f, t2ji = 0.f, t3ji = 0.f;
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) {
+      const float vi = expf(li[k]), vj = expf(lj[k]);
+      const float df = mj[k] - mi[k];
+      const float D = df * df;
+      Li += li[k];
+      Lj += lj[k];
+      t2ij += D / vj;
+      t3ij += vj / (vi + 1e-8f);
+      t2ji += D / vi;
+      t3ji += vi / (vj + 1e-8f);
+    }
+  const float kij = 0.5f * ((Lj - Li - (float)d) + t2ij + t3ij);
+  const float kji = 0.5f * ((Li - Lj - (float)d) + t2ji + t3ji);
+  return -(0.5f * (kij + kji));
+}
+
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) {
+    m = mn;
+    s = 0.f;
+    return;
+  }
+  s = s * expf(m - mn) + s2 * expf(m2 - mn);
+  m = mn;
+}
+
+template <int DM>
+__device__ __forceinline__ void load_theta(const Branch& b, int r, int d, float* m, float* l, bool need_lv) {
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    m[k] = (k < d) ? b.mu[(size_t)r * b.ld + k] : 0.f;
+    l[k] = (need_lv && k < d) ? b.lv[(size_t)r * b.ld + k] : 0.f;
+  }
+}
+
+__device__ __forceinline__ float row_norm(const Branch& b, int r, int d) {
+  float s = 0.f;
+  for (int k = 0; k < d; ++k) {
+    const float v = b.mu[(size_t)r * b.ld + k];
+    s += v * v;
+  }
+  return sqrtf(s);
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void ntxent_rows_kernel(const NtArgs A) {
+  __shared__ float nrm[NT_MAXN];
+  const Branch& b = A.br[blockIdx.y];
+  const int n = A.n, d = A.d;
+  const bool cosine = A.sim == CV_SIM_COSINE;
+  const bool need_lv = !(A.sim == CV_SIM_COSINE || A.sim == CV_SIM_L2);
+  if (cosine)
+    for (int j = threadIdx.x; j < n; j += 256) nrm[j] = fmaxf(row_norm(b, j, d), 1e-8f);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * NT_ROWS + w;
+  if (i >= n) return;
+  float mi[DM], li[DM], mj[DM], lj[DM];
+  load_theta<DM>(b, i, d, mi, li, need_lv);
+  const float ni = cosine ? nrm[i] : 1.f;
+  const int64_t lab = A.label[i];
+  float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    if (j == i) continue;
+    load_theta<DM>(b, j, d, mj, lj, need_lv);
+    const float s = sim_ij<DM>(A.sim, mi, li, ni, mj, lj, cosine ? nrm[j] : 1.f, d) / A.tau;
+    lse_merge(ma, sa, s, 1.f);
+    const bool pos = b.ps ? (A.label[j] != lab) : (A.label[j] == lab);
+    if (pos) lse_merge(mp, sp, s, 1.f);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(ma, o, 64), s2 = __shfl_xor(sa, o, 64);
+    const float m3 = __shfl_xor(mp, o, 64), s3 = __shfl_xor(sp, o, 64);
+    lse_merge(ma, sa, m2, s2);
+    lse_merge(mp, sp, m3, s3);
+  }
+  if (lane == 0) {
+    b.lse[i] = (sa > 0.f) ? ma + logf(sa) : -INFINITY;
+    b.lse[n + i] = (sp > 0.f) ? mp + logf(sp) : -INFINITY;
+  }
+}
+
+// d S_ij / d theta_i (row derivative), accumulated with weight H
+template <int DM>
+__device__ __forceinline__ void sim_grad_row(int sim, const float* mi, const float* li, float ni, bool clamped_i,
+                                             const float* mj, const float* lj, float nj, float S, float H, int d,
+                                             float* gm, float* gl) {
+  if (sim == CV_SIM_COSINE) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) {
+        const float uj = mj[k] / nj, ui = mi[k] / ni;
+        gm[k] += H * (clamped_i ? uj : (uj - S * ui)) / ni;
+      }
+    return;
+  }
+  if (sim == CV_SIM_L2) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) gm[k] += H * 2.f * (mj[k] - mi[k]);
+    return;
+  }
+  if (sim == CV_SIM_MODIFIED_L2) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) {
+        const float df = mj[k] - mi[k];
+        const float V = expf(0.5f * (lj[k] + li[k]));
+        gm[k] += H * 2.f * df / V;
+        gl[k] += H * 0.5f * df * df / V;
+      }
+    return;
+  }
+  if (sim == CV_SIM_MAHALANOBIS) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) {
+        const float df = mj[k] - mi[k];
+        const float vi = expf(li[k]);
+        const float V = 0.5f * (expf(lj[k]) + vi);
+        gm[k] += H * 2.f * df / V;
+        gl[k] += H * df * df / (V * V) * 0.5f * vi;
+      }
+    return;
+  }
+  // jeffrey
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) {
+      const float vi = expf(li[k]), vj = expf(lj[k]);
+      const float df = mj[k] - mi[k];
+      const float D = df * df;
+      gm[k] += H * 0.5f * df * (1.f / vj + 1.f / vi);
+      const float a = vi + 1e-8f;
+      gl[k] += H * (-0.25f) * (-(vj * vi) / (a * a) - D / vi + vi / (vj + 1e-8f));
+    }
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void ntxent_grad_kernel(const NtArgs A) {
+  __shared__ float nrm[NT_MAXN];
+  __shared__ float rawn[NT_MAXN];
+  __shared__ float scratch[16];
+  __shared__ double dscratch[16];
+  const Branch& b = A.br[blockIdx.y];
+  const int n = A.n, d = A.d;
+  const bool cosine = A.sim == CV_SIM_COSINE;
+  const bool need_lv = !(A.sim == CV_SIM_COSINE || A.sim == CV_SIM_L2);
+  // finite-row count (and, in block 0, the loss)
+  float cnt = 0.f;
+  double lsum = 0.0;
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const float l = b.lse[j] - b.lse[n + j];
+    if (isfinite(l)) {
+      cnt += 1.f;
+      lsum += (double)l;
+    }
+    if (cosine) {
+      const float r = row_norm(b, j, d);
+      rawn[j] = r;
+      nrm[j] = fmaxf(r, 1e-8f);
+    }
+  }
+  const float nf = block_sum<256>(cnt, scratch);
+  if (blockIdx.x == 0) {
+    const double tot = block_sum<256>(lsum, dscratch);
+    if (threadIdx.x == 0 && b.loss_out) b.loss_out[0] = (nf > 0.f) ? (float)(tot / (double)nf) : NAN;
+  }
+  __syncthreads();
+  if (!b.dmu) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * NT_ROWS + w;
+  if (i >= n) return;
+  const float gup = b.gmul * (b.gscale ? b.gscale[0] : 1.0f);
+  const float c = (nf > 0.f) ? gup / (nf * A.tau) : 0.f;
+  float mi[DM], li[DM], mj[DM], lj[DM], gm[DM], gl[DM];
+  load_theta<DM>(b, i, d, mi, li, need_lv);
+#pragma unroll
+  for (int k = 0; k < DM; ++k) { gm[k] = 0.f; gl[k] = 0.f; }
+  const float ni = cosine ? nrm[i] : 1.f;
+  const bool clamped_i = cosine && !(rawn[i] > 1e-8f);
+  const int64_t lab = A.label[i];
+  const float la_i = b.lse[i], lp_i = b.lse[n + i];
+  const bool fin_i = isfinite(la_i - lp_i);
+  for (int j = lane; j < n; j += 64) {
+    if (j == i) continue;
+    load_theta<DM>(b, j, d, mj, lj, need_lv);
+    const float nj = cosine ? nrm[j] : 1.f;
+    const float S = sim_ij<DM>(A.sim, mi, li, ni, mj, lj, nj, d);
+    const float s = S / A.tau;
+    const bool pos = b.ps ? (A.label[j] != lab) : (A.label[j] == lab);
+    const float la_j = b.lse[j], lp_j = b.lse[n + j];
+    const bool fin_j = isfinite(la_j - lp_j);
+    float G = 0.f;
+    if (fin_i) G += c * (expf(s - la_i) - (pos ? expf(s - lp_i) : 0.f));
+    if (fin_j) G += c * (expf(s - la_j) - (pos ? expf(s - lp_j) : 0.f));
+    if (G != 0.f) sim_grad_row<DM>(A.sim, mi, li, ni, clamped_i, mj, lj, nj, S, G, d, gm, gl);
+  }
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    if (k < d) {
+      gm[k] = wave_sum(gm[k]);
+      if (need_lv) gl[k] = wave_sum(gl[k]);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < DM; ++k) {
+      if (k < d) {
+        float* pm = b.dmu + (size_t)i * b.gld + k;
+        *pm = A.accumulate ? *pm + gm[k] : gm[k];
+        if (b.dlv) {
+          float* pl = b.dlv + (size_t)i * b.gld + k;
+          const float v = need_lv ? gl[k] : 0.f;
+          *pl = A.accumulate ? *pl + v : v;
+        }
+      }
+    }
+  }
+}
+
+template <template <int> class K>
+struct DDispatch;
+
+static int ntxent_launch(const NtArgs& a, int nbr, bool rows, hipStream_t st) {
+  dim3 grid(cdiv(a.n, NT_ROWS), nbr);
+  if (a.d <= 8) {
+    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<8>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(ntxent_grad_kernel<8>, grid, dim3(256), 0, st, a);
+  } else if (a.d <= 16) {
+    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<16>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(ntxent_grad_kernel<16>, grid, dim3(256), 0, st, a);
+  } else if (a.d <= 32) {
+    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<32>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(ntxent_grad_kernel<32>, grid, dim3(256), 0, st, a);
+  } else {
+    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<64>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(ntxent_grad_kernel<64>, grid, dim3(256), 0, st, a);
+  }
+  CV_LAUNCH_CHECK(rows ? "ntxent_rows" : "ntxent_grad");
+  return 0;
+}
+
+}  // namespace cv
+
+using namespace cv;
+
+extern "C" int cv_reparam_forward(const float* heads, int n, int d, const float* eps, uint64_t seed, uint64_t* offset,
+                                  float* z, float* eps_out, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(heads && z && n > 0 && d > 0, "reparam_forward: bad args");
+  CV_REQUIRE(eps || offset, "reparam_forward: need injected eps or a device offset counter");
+  hipLaunchKernelGGL(reparam_kernel, dim3(1), dim3(1024), 0, S(stream), heads, n, d, eps, seed, offset, z, eps_out);
+  CV_LAUNCH_CHECK("reparam_forward");
+  return 0;
+}
+
+extern "C" int cv_sample_forward(const float* mu, const float* logvar, long numel, const float* eps, uint64_t seed,
+                                 uint64_t* offset, float* z, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(mu && logvar && z && numel > 0, "sample_forward: bad args");
+  CV_REQUIRE(eps || offset, "sample_forward: need injected eps or a device offset counter");
+  long g = (numel / 2 + 255) / 256 + 1;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(sample_kernel, dim3(g), dim3(256), 0, S(stream), mu, logvar, numel, eps, seed,
+                     eps ? nullptr : offset, z);
+  CV_LAUNCH_CHECK("sample_forward");
+  return 0;
+}
+
+extern "C" int cv_sample_backward(const float* mu, const float* z, const float* dz, long numel, float* dmu,
+                                  float* dlogvar, int accumulate, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(mu && z && dz && dmu && dlogvar && numel > 0, "sample_backward: bad args");
+  long g = (numel + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(sample_bwd_kernel, dim3(g), dim3(256), 0, S(stream), mu, z, dz, numel, dmu, dlogvar,
+                     accumulate);
+  CV_LAUNCH_CHECK("sample_backward");
+  return 0;
+}
+
+extern "C" int cv_kl(const float* mu, const float* logvar, int ld, int n, int d, float* kl_out, const float* gscale,
+                     float* dmu, float* dlogvar, int gld, int accumulate, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(mu && logvar && n > 0 && d > 0, "kl: bad args");
+  CV_REQUIRE(!dmu == !dlogvar, "kl: dmu and dlogvar go together");
+  hipLaunchKernelGGL(kl_kernel, dim3(1), dim3(1024), 0, S(stream), mu, logvar, ld, n, d, kl_out, gscale, dmu, dlogvar,
+                     gld, accumulate);
+  CV_LAUNCH_CHECK("kl");
+  return 0;
+}
+
+extern "C" int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
+                                 float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                                 float* dheads, float* losses, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine: bad args");
+  hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), heads, z, dz, n, d, beta, loc, scale,
+                     anneal_step, rec_in, dheads, losses);
+  CV_LAUNCH_CHECK("latent_combine");
+  return 0;
+}
+
+extern "C" int cv_mse_sum(const float* xhat, const float* x, int n, int per_sample, float* rec_out,
+                          const float* gscale, float* dxhat, double* work, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(xhat && x && n > 0 && per_sample > 0, "mse_sum: bad args");
+  const long total = (long)n * per_sample;
+  long g = (total + 1023) / 1024;
+  if (g > 512) g = 512;
+  if (rec_out) {
+    CV_REQUIRE(work != nullptr, "mse_sum: forward needs a zeroed fp64 work word");
+    hipLaunchKernelGGL(mse_kernel, dim3(g), dim3(1024), 0, S(stream), xhat, x, total, n, rec_out, work);
+    hipLaunchKernelGGL(mse_finish_kernel, dim3(1), dim3(64), 0, S(stream), work, n, rec_out);
+  }
+  if (dxhat) {
+    long g2 = (total + 255) / 256;
+    if (g2 > 2048) g2 = 2048;
+    hipLaunchKernelGGL(mse_bwd_kernel, dim3(g2), dim3(256), 0, S(stream), xhat, x, total, n, gscale, dxhat);
+  }
+  CV_LAUNCH_CHECK("mse_sum");
+  return 0;
+}
+
+extern "C" int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
+                         float temperature, int phase, int accumulate, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(br && nbr >= 1 && nbr <= MAXBR && label && n > 0 && d > 0 && d <= 64, "ntxent: bad args (d<=64)");
+  CV_REQUIRE(n <= NT_MAXN, "ntxent: batch %d > %d", n, NT_MAXN);
+  CV_REQUIRE(sim >= CV_SIM_COSINE && sim <= CV_SIM_MAHALANOBIS, "unimplemented similarity measure.");
+  NtArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int i = 0; i < nbr; ++i) {
+    CV_REQUIRE(br[i].mu && br[i].lse, "ntxent: branch %d incomplete", i);
+    const bool need_lv = !(sim == CV_SIM_COSINE || sim == CV_SIM_L2);
+    CV_REQUIRE(!need_lv || br[i].logvar, "ntxent: this similarity needs logvar");
+    a.br[i].mu = br[i].mu;
+    a.br[i].lv = br[i].logvar;
+    a.br[i].ld = br[i].ld;
+    a.br[i].ps = br[i].ps;
+    a.br[i].dmu = br[i].dmu;
+    a.br[i].dlv = br[i].dlogvar;
+    a.br[i].gld = br[i].gld;
+    a.br[i].gscale = br[i].gscale;
+    a.br[i].gmul = br[i].gmul;
+    a.br[i].loss_out = br[i].loss_out;
+    a.br[i].lse = br[i].lse;
+  }
+  a.label = label;
+  a.n = n;
+  a.d = d;
+  a.sim = sim;
+  a.tau = temperature;
+  a.accumulate = accumulate;
+  if (phase == 0 || phase == 2) {
+    if (ntxent_launch(a, nbr, true, S(stream))) return 2;
+  }
+  if (phase == 1 || phase == 2) {
+    if (ntxent_launch(a, nbr, false, S(stream))) return 2;
+  }
+  return 0;
+}

@@ -1,0 +1,254 @@
+"""ctypes binding of libclearvae_hip.so (the C-ABI declared in include/clearvae.h).
+
+Every struct below mirrors include/clearvae.h field for field.  The library is loaded after
+``import torch`` so that it binds to the HIP runtime torch already loaded (same SONAME), which is
+what makes torch's device pointers and ``torch.cuda.current_stream().cuda_stream`` valid here.
+
+There is deliberately no CPU fallback: if the shared object is missing or cannot be loaded,
+:func:`lib` raises, and every op that needs it fails loudly.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_int64, c_size_t, c_uint64, c_void_p
+
+import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libclearvae_hip.so")
+
+STAT_REPL = 8
+
+XF_NONE, XF_BNRELU, XF_BNBWD = 0, 1, 2
+STAT_NONE, STAT_FWD, STAT_BWD = 0, 1, 2
+SIM = {"cosine": 0, "l2": 1, "modified_l2": 2, "jeffrey": 3, "mahalanobis": 4}
+MI_NONE, MI_CLUBSAMPLE, MI_L1OUT = 0, 1, 2
+
+
+class cv_bn(ctypes.Structure):
+    _fields_ = [
+        ("gamma", c_void_p),
+        ("beta", c_void_p),
+        ("stat", c_void_p),
+        ("gstat", c_void_p),
+        ("running_mean", c_void_p),
+        ("running_var", c_void_p),
+        ("C", c_int),
+        ("count", c_int),
+        ("train", c_int),
+        ("eps", c_float),
+    ]
+
+
+class cv_operand(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("xf", c_int), ("nchw", c_int), ("bn", cv_bn)]
+
+
+class cv_epilogue(ctypes.Structure):
+    _fields_ = [
+        ("stat_mode", c_int),
+        ("stat_out", c_void_p),
+        ("stat_div", c_int),
+        ("ey", c_void_p),
+        ("ebn", cv_bn),
+        ("erelu", c_int),
+    ]
+
+
+class cv_conv(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int),
+        ("c_in", c_int),
+        ("h_in", c_int),
+        ("w_in", c_int),
+        ("c_out", c_int),
+        ("h_out", c_int),
+        ("w_out", c_int),
+        ("kh", c_int),
+        ("kw", c_int),
+        ("stride", c_int),
+        ("pad", c_int),
+        ("transposed", c_int),
+    ]
+
+
+class cv_linear(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int),
+        ("in_features", c_int),
+        ("out_features", c_int),
+        ("in_pix", c_int),
+        ("in_ch", c_int),
+        ("out_pix", c_int),
+        ("out_ch", c_int),
+    ]
+
+
+class cv_ntxent_branch(ctypes.Structure):
+    _fields_ = [
+        ("mu", c_void_p),
+        ("logvar", c_void_p),
+        ("ld", c_int),
+        ("ps", c_int),
+        ("dmu", c_void_p),
+        ("dlogvar", c_void_p),
+        ("gld", c_int),
+        ("gscale", c_void_p),
+        ("gmul", c_float),
+        ("loss_out", c_void_p),
+        ("lse", c_void_p),
+    ]
+
+
+class cv_mlp(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4")] + [
+        ("dx", c_int),
+        ("h", c_int),
+        ("dy", c_int),
+    ]
+
+
+class cv_mlp_grad(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4")]
+
+
+_P = POINTER
+# name -> (restype, argtypes)
+_SIGS = {
+    "cv_conv_forward": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
+    "cv_conv_backward_data": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
+    "cv_conv_backward_weight": (
+        c_int,
+        [_P(cv_conv), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p],
+    ),
+    "cv_linear_forward": (
+        c_int,
+        [_P(cv_linear), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_int, _P(cv_epilogue), c_void_p],
+    ),
+    "cv_linear_backward_data": (
+        c_int,
+        [_P(cv_linear), _P(cv_operand), c_void_p, c_void_p, c_int, _P(cv_epilogue), c_void_p],
+    ),
+    "cv_linear_backward_weight": (
+        c_int,
+        [_P(cv_linear), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p],
+    ),
+    "cv_declinear_backward_weight": (
+        c_int,
+        [_P(cv_linear), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_bn_apply": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "cv_bn_update_running": (c_int, [_P(cv_bn), c_int, c_float, _P(c_void_p), c_void_p]),
+    "cv_bn_batch_stats": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_void_p]),
+    "cv_output_forward": (c_int, [_P(cv_bn), c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "cv_output_loss": (
+        c_int,
+        [_P(cv_bn), c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p],
+    ),
+    "cv_output_backward": (
+        c_int,
+        [_P(cv_bn), c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_reparam_forward": (
+        c_int,
+        [c_void_p, c_int, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_sample_forward": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_uint64, c_void_p, c_void_p,
+                                  c_void_p]),
+    "cv_sample_backward": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p, c_int,
+                                   c_void_p]),
+    "cv_kl": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    ),
+    "cv_latent_combine": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p],
+    ),
+    "cv_mse_sum": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cv_ntxent": (
+        c_int,
+        [_P(cv_ntxent_branch), c_int, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
+    ),
+    "cv_mi_workspace_bytes": (c_size_t, [c_int]),
+    "cv_mi_forward": (
+        c_int,
+        [c_int, _P(cv_mlp), c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_uint64, c_void_p, c_void_p,
+         c_void_p, c_void_p],
+    ),
+    "cv_mi_backward": (
+        c_int,
+        [c_int, _P(cv_mlp), c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p,
+         c_void_p, c_int, c_int, _P(cv_mlp_grad), c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    ),
+    "cv_mi_learning_step": (
+        c_int,
+        [_P(cv_mlp), c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, _P(cv_mlp_grad), c_void_p, c_void_p,
+         c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_adam_step": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_bn_param_grads": (c_int, [_P(cv_bn), c_int, _P(c_void_p), _P(c_void_p), c_void_p]),
+    "cv_zero": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "cv_last_error": (ctypes.c_char_p, []),
+    "cv_version": (c_int, []),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_LIB = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared object and declare every prototype (no GPU needed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise HipLibraryError(
+            f"libclearvae_hip.so not found at {path}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def lib():
+    return load()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _LIB.cv_last_error().decode() if _LIB is not None else "?"
+        raise RuntimeError(f"{what}: {msg}")
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream

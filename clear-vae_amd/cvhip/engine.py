@@ -1,0 +1,346 @@
+"""Fused CLEAR training step: one HIP program per step, replayed as a HIP graph.
+
+ClearStep runs the body of CLEARVAETrainer._train (code/src/trainer.py:447-484) or of
+ClearMIMVAETrainer._train (code/src/trainer.py:842-888) as a fixed sequence of libclearvae_hip.so
+calls over device-resident buffers:
+
+  zero(stats, grads) -> encoder (conv + fused BN/ReLU) -> heads -> reparam -> decoder -> output BN +
+  sigmoid + reconstruction loss + backward seed -> decoder backward -> KL / contrastive / MI
+  gradients into d(heads) -> heads + encoder backward -> BN affine grads -> [RCCL all-reduce] ->
+  Adam on the flat parameter arena (+ LogisticAnnealer step on the device)
+
+For CLEAR-MIM the 5 estimator updates follow (each: a train-mode forward for BN statistics and z,
+then one fused learning-loss + Adam kernel on the estimator arena).
+
+The first step at a new batch size runs eagerly (it also loads the code objects); the second is
+captured into a torch.cuda.CUDAGraph and every later step replays it.  Step-varying scalars (RNG
+offset, Adam step, annealer step) live in device counters advanced by the kernels, so replays need
+no host writes.  Host-visible PyTorch state (param .data / .grad, optimizer.state exp_avg /
+exp_avg_sq, BN running stats) are views of, or are updated in place by, the same device buffers;
+the optimizer's CPU 'step' counters are synchronised at the end of every epoch (sync_host_state).
+
+Data parallel: when torch.distributed is initialised with world_size > 1 the gradient arena is
+all-reduced (RCCL over xGMI) between the backward graph and the Adam graph, in two buckets so the
+decoder bucket (ready first) overlaps the encoder backward on a side stream.  Semantics are those
+of torch DDP around the reference (local-batch BN / contrastive / MI terms, averaged gradients).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib, rng
+from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
+from .autograd import est_params, mlp_struct
+from .plan import ParamArena, Program, Workspace, ensure_arena
+
+
+def _dist_world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
+class _AdamState:
+    """Flat Adam state bound to a torch.optim.Adam over exactly the params of `arena`."""
+
+    def __init__(self, optimizer, arena: ParamArena):
+        self.opt = optimizer
+        self.arena = arena
+        dev = arena.device
+        self.m = torch.zeros(arena.numel, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(arena.numel, dtype=torch.float32, device=dev)
+        steps = 0
+        with torch.no_grad():
+            for p in arena.params:
+                st = optimizer.state.get(p, {})
+                if "exp_avg" in st:
+                    o, n = arena.offset[id(p)]
+                    self.m[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                    self.v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    steps = int(float(st["step"]))
+        self.host_steps = steps
+        self.step = torch.tensor([steps, 0], dtype=torch.int64, device=dev)
+        self.hyper_host = None
+        self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.refresh_hyper()
+        # bind optimizer.state to views of the flat state
+        for p in arena.params:
+            o, n = arena.offset[id(p)]
+            optimizer.state[p] = {
+                "step": torch.tensor(float(steps)),
+                "exp_avg": self.m[o:o + n].view_as(p),
+                "exp_avg_sq": self.v[o:o + n].view_as(p),
+            }
+
+    @staticmethod
+    def supported(optimizer, params) -> bool:
+        if type(optimizer) is not torch.optim.Adam or len(optimizer.param_groups) != 1:
+            return False
+        g = optimizer.param_groups[0]
+        if g.get("amsgrad") or g.get("maximize") or g.get("differentiable") or g.get("decoupled_weight_decay"):
+            return False
+        if isinstance(g["lr"], torch.Tensor) or isinstance(g["betas"][0], torch.Tensor):
+            return False
+        ids = {id(p) for p in g["params"]}
+        if ids != {id(p) for p in params} or not all(p.requires_grad for p in params):
+            return False
+        return True
+
+    def refresh_hyper(self):
+        g = self.opt.param_groups[0]
+        h = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
+        if h != self.hyper_host:
+            self.hyper_host = h
+            self.hyper.copy_(torch.tensor(list(h) + [0.0, 0.0, 0.0], dtype=torch.float32))
+
+    def sync_host(self, n_new: int):
+        self.host_steps += n_new
+        for p in self.arena.params:
+            st = self.opt.state[p]
+            st["step"] = torch.tensor(float(self.host_steps))
+
+
+class ClearStep:
+    @classmethod
+    def build(cls, trainer, mode: str):
+        """Return a fused step for `trainer`, or None when its setup is outside the fused contract."""
+        vae = trainer.model
+        try:
+            dev = next(vae.parameters()).device
+        except StopIteration:
+            return None
+        if dev.type != "cuda" or trainer.transform is not None:
+            return None
+        try:
+            arena = ensure_arena(vae)
+        except (NotImplementedError, AssertionError):
+            return None
+        if not _AdamState.supported(trainer.optimizer, arena.params):
+            return None
+        sim = trainer.sim_fn
+        if sim not in SIM:
+            raise ValueError("unimplemented similarity measure.")
+        if mode == "mim":
+            from src.models.mi_estimator import CLUBSample, L1OutUB
+
+            est = trainer.mi_estimator
+            if type(est) not in (CLUBSample, L1OutUB):
+                return None
+            if not _AdamState.supported(trainer.mi_estimator_optimizer, est_params(est)):
+                return None
+        return cls(trainer, mode)
+
+    def __init__(self, trainer, mode: str):
+        self.trainer = trainer
+        self.mode = mode
+        self.vae = trainer.model
+        self.arena = ensure_arena(self.vae)
+        self.spec = self.vae._cv_spec
+        self.device = self.arena.device
+        self.adam = _AdamState(trainer.optimizer, self.arena)
+        hp = trainer.hyperparameter
+        self.hp = dict(hp)
+        self.sim = SIM[trainer.sim_fn]
+        self.anneal = torch.tensor([trainer.annealer.current_step], dtype=torch.int64, device=self.device)
+        self.seed, _ = rng.offset_tensor(self.device)
+        self.offset = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self.world = _dist_world()
+        self.gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
+        self.graphs = {}  # n -> dict
+        self.steps_since_sync = 0
+        if mode == "mim":
+            self.est = trainer.mi_estimator
+            self.est_arena = ParamArena(est_params(self.est), self.device)
+            self.est_adam = _AdamState(trainer.mi_estimator_optimizer, self.est_arena)
+            self.kind = MI_CLUBSAMPLE if type(self.est).__name__ == "CLUBSample" else MI_L1OUT
+            self.learn = torch.zeros(5, dtype=torch.float32, device=self.device)
+        # grads visible through p.grad (like the reference after loss.backward())
+        for p in self.arena.params:
+            p.grad = self.arena.gview(p)
+        self._sig = self._signature()
+
+    # ----------------------------------------------------------------------------- bookkeeping
+    def _signature(self):
+        t = self.trainer
+        sig = (id(t.optimizer), t.sim_fn, tuple(sorted((k, str(v)) for k, v in t.hyperparameter.items())))
+        if self.mode == "mim":
+            sig += (id(t.mi_estimator), id(t.mi_estimator_optimizer))
+        return sig
+
+    def compatible(self) -> bool:
+        if self._signature() != self._sig or not self.arena.valid():
+            return False
+        if self.mode == "mim" and not self.est_arena.valid():
+            return False
+        if self.anneal_host() != self.trainer.annealer.current_step:
+            self.anneal.fill_(self.trainer.annealer.current_step)
+        return True
+
+    def anneal_host(self):
+        return self.trainer.annealer.current_step  # device counter mirrors the host one (same increments)
+
+    def accepts(self, X) -> bool:
+        sp = self.spec
+        return (X.device.type == "cuda" and X.dim() == 4 and tuple(X.shape[1:]) == (sp.in_ch, sp.H, sp.W)
+                and X.shape[0] >= 2)
+
+    def sync_host_state(self):
+        if self.steps_since_sync:
+            self.adam.sync_host(self.steps_since_sync)
+            if self.mode == "mim":
+                self.est_adam.sync_host(5 * self.steps_since_sync)
+            self.steps_since_sync = 0
+
+    # ----------------------------------------------------------------------------- programs
+    def _programs(self, n: int):
+        sp = self.spec
+        ws = Workspace(sp, n, self.device, with_grad=True)
+        X = torch.empty(n, sp.in_ch, sp.H, sp.W, dtype=torch.float32, device=self.device)
+        lab = torch.zeros(n, dtype=torch.int64, device=self.device)
+        A = self.arena
+        hp = self.hp
+        d = sp.d
+        pg = A.gptr
+        fwd = Program()
+        fwd.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+        fwd.add("cv_zero", A.grad, A.numel * 4)
+        ws.encoder_program(fwd, X, True)
+        ws.reparam_program(fwd, None, self.seed, self.offset)
+        ws.decoder_program(fwd, ws.z, True, "loss", X)
+        ws.running_program(fwd, "all")
+        # decoder backward (bucket 1 of the gradient arena)
+        dec = Program()
+        ws.decoder_backward_program(dec, pg, ws.dz)
+        ws.bn_grads_program(dec, pg, "dec")
+        # latent terms -> d(heads)
+        lat = Program()
+        lat.add("cv_latent_combine", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
+                ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
+                ws.scal[0:1], ws.dheads, ws.losses)
+        hb = ws.heads.data_ptr()
+        dh = ws.dheads.data_ptr()
+        alpha = float(hp["alpha"])
+        tau = float(hp["temperature"])
+        branches = [cv_ntxent_branch(hb, hb + 4 * d, 4 * d, 0, dh, dh + 4 * d, 4 * d, None, alpha,
+                                     ws.losses.data_ptr() + 12, ws.lse[0].data_ptr())]
+        if self.mode == "clear":
+            ps = bool(hp["ps"])
+            branches.append(cv_ntxent_branch(hb + 8 * d, hb + 12 * d, 4 * d, int(ps), dh + 8 * d, dh + 12 * d, 4 * d,
+                                             None, alpha if ps else -alpha, ws.losses.data_ptr() + 16,
+                                             ws.lse[1].data_ptr()))
+        arr = (cv_ntxent_branch * len(branches))(*branches)
+        lat.add("cv_ntxent", arr, len(branches), lab, n, d, self.sim, ctypes.c_float(tau), 2, 1)
+        if self.mode == "mim":
+            mlp = mlp_struct(self.est)
+            zp = ws.z.data_ptr()
+            lat.add("cv_mi_forward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, None, ctypes.c_uint64(self.seed),
+                    self.offset, ws.mi_work, ws.losses.data_ptr() + 20)
+            lat.add("cv_mi_backward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work, None,
+                    ctypes.c_float(float(hp["lambda"])), None, None, 0, 1, None, ws.heads, ws.z, ws.dheads, d)
+        enc = Program()
+        ws.encoder_backward_program(enc, pg, ws.dheads, x=X)
+        ws.bn_grads_program(enc, pg, "enc")
+        upd = Program()
+        upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper, self.adam.step,
+                self.gscale if self.world > 1 else None, self.anneal)
+        learn = None
+        if self.mode == "mim":
+            learn = Program()
+            E = self.est_arena
+            mlp = mlp_struct(self.est)
+            G = cv_mlp_grad(*[E.gptr(p) for p in est_params(self.est)])
+            zp = ws.z.data_ptr()
+            for j in range(5):
+                learn.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+                ws.encoder_program(learn, X, True)
+                ws.reparam_program(learn, None, self.seed, self.offset)
+                ws.decoder_program(learn, ws.z, True, "none")
+                ws.running_program(learn, "all")
+                learn.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n,
+                          self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
+                          E.numel, self.est_adam.hyper, self.est_adam.step)
+        return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, upd=upd, learn=learn)
+
+    def _bucket_split(self):
+        """Offset of the first decoder parameter in the arena (decoder grads = [split, numel))."""
+        sp = self.spec
+        return self.arena.offset[id(sp.dec_lin.weight)][0]
+
+    def _run_eager(self, G):
+        s = _lib.stream_handle()
+        G["fwd"].run(s)
+        G["dec"].run(s)
+        G["lat"].run(s)
+        G["enc"].run(s)
+        self._reduce()
+        G["upd"].run(s)
+        if G["learn"] is not None:
+            G["learn"].run(s)
+
+    def _reduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.arena.grad)
+
+    def _capture(self, G):
+        if self.world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                s = _lib.stream_handle()
+                for k in ("fwd", "dec", "lat", "enc", "upd"):
+                    G[k].run(s)
+                if G["learn"] is not None:
+                    G["learn"].run(s)
+            G["graphs"] = [g]
+        else:
+            # backward graph / [all-reduce] / update graph
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                s = _lib.stream_handle()
+                for k in ("fwd", "dec", "lat", "enc"):
+                    G[k].run(s)
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                s = _lib.stream_handle()
+                G["upd"].run(s)
+                if G["learn"] is not None:
+                    G["learn"].run(s)
+            G["graphs"] = [g1, g2]
+
+    # ----------------------------------------------------------------------------- one step
+    def step(self, X, label):
+        n = X.shape[0]
+        G = self.graphs.get(n)
+        if G is None:
+            G = self._programs(n)
+            G["count"] = 0
+            self.graphs[n] = G
+        self.adam.refresh_hyper()
+        if self.mode == "mim":
+            self.est_adam.refresh_hyper()
+        G["X"].copy_(X, non_blocking=True)
+        G["lab"].copy_(label.reshape(-1), non_blocking=True)
+        use_graph = G["count"] >= 1 and not rng.pending_noise()
+        if use_graph and "graphs" not in G:
+            self._capture(G)
+        if use_graph:
+            if self.world == 1:
+                G["graphs"][0].replay()
+            else:
+                G["graphs"][0].replay()
+                self._reduce()
+                G["graphs"][1].replay()
+        else:
+            self._run_eager(G)
+        G["count"] += 1
+        self.steps_since_sync += 1
+        ws = G["ws"]
+        if self.mode == "mim":
+            return ws.losses, self.learn.clone()
+        return ws.losses
+
+    def last_workspace(self, n):
+        return self.graphs[n]["ws"]

@@ -1,0 +1,505 @@
+"""Layer plan of a CLEAR-VAE model on the HIP kernels.
+
+``VaeSpec`` reads the topology of a ``VAE`` / ``VAE64`` module (code/src/models/vae.py:7-156 of the
+reference): the conv encoder, the four latent heads, the decoder Linear -> BatchNorm1d -> ReLU ->
+Unflatten, the transposed-conv decoder and the BatchNorm + Sigmoid output.
+
+``ParamArena`` moves every parameter of a module into one flat fp32 buffer (params become views), so
+the whole model's gradient, Adam state and data-parallel all-reduce are single contiguous buffers.
+
+``Workspace`` holds the per-batch-size device buffers (NHWC activations, gradients, fp64 BatchNorm
+statistics) and ``Program`` a pre-built list of C-ABI calls over them; the fused trainer captures a
+program into a HIP graph, the autograd path runs it eagerly.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import (
+    STAT_BWD,
+    STAT_FWD,
+    STAT_NONE,
+    STAT_REPL,
+    XF_BNBWD,
+    XF_BNRELU,
+    XF_NONE,
+    cv_bn,
+    cv_conv,
+    cv_epilogue,
+    cv_linear,
+    cv_operand,
+)
+
+# ----------------------------------------------------------------------------- topology
+
+
+@dataclass
+class ConvSpec:
+    mod: nn.Module  # nn.Conv2d or nn.ConvTranspose2d
+    bn: nn.Module  # BatchNorm2d after it
+    relu: bool  # ReLU after the BN (False for the decoder output: Sigmoid)
+    transposed: bool
+    c_in: int
+    h_in: int
+    w_in: int
+    c_out: int
+    h_out: int
+    w_out: int
+
+    def geom(self, n: int) -> cv_conv:
+        m = self.mod
+        return cv_conv(
+            n, self.c_in, self.h_in, self.w_in, self.c_out, self.h_out, self.w_out,
+            m.kernel_size[0], m.kernel_size[1], m.stride[0], m.padding[0], int(self.transposed),
+        )
+
+
+@dataclass
+class VaeSpec:
+    in_ch: int
+    H: int
+    W: int
+    d: int  # z_dim (per factor)
+    enc: list
+    heads: list  # [mu_c, logvar_c, mu_s, logvar_s] nn.Linear
+    feat: tuple  # (C, H, W) of the flattened encoder output
+    dec_lin: nn.Linear
+    dec_bn: nn.BatchNorm1d
+    unflat: tuple  # (C, H, W) of the decoder Linear output
+    dec: list = field(default_factory=list)
+
+    @property
+    def F(self) -> int:
+        c, h, w = self.feat
+        return c * h * w
+
+    @property
+    def bn_layers(self) -> list:
+        return [c.bn for c in self.enc] + [self.dec_bn] + [c.bn for c in self.dec]
+
+
+def _conv_out(h, k, s, p):
+    return (h + 2 * p - k) // s + 1
+
+
+def _convT_out(h, k, s, p, op):
+    return (h - 1) * s - 2 * p + k + op
+
+
+def vae_spec(vae: nn.Module, image_hw: int | None = None) -> VaeSpec:
+    """Derive the layer plan from the module tree (the attribute names of the reference VAE)."""
+    enc_mods = list(vae.encoder)
+    in_ch = None
+    for m in enc_mods:
+        if isinstance(m, nn.Conv2d):
+            in_ch = m.in_channels
+            break
+    # image size: VAE (k=3) is 28x28; VAE64 (k=4) is 64x64 (Linear(2048) fixes both)
+    first = next(m for m in enc_mods if isinstance(m, nn.Conv2d))
+    if image_hw is None:
+        image_hw = 28 if first.kernel_size[0] == 3 else 64
+    h = w = image_hw
+    c = in_ch
+    enc = []
+    i = 0
+    while i < len(enc_mods):
+        m = enc_mods[i]
+        if isinstance(m, nn.Conv2d):
+            bn = enc_mods[i + 1]
+            assert isinstance(bn, nn.BatchNorm2d) and isinstance(enc_mods[i + 2], nn.ReLU), "unexpected encoder"
+            k, s, p = m.kernel_size[0], m.stride[0], m.padding[0]
+            ho, wo = _conv_out(h, k, s, p), _conv_out(w, k, s, p)
+            enc.append(ConvSpec(m, bn, True, False, c, h, w, m.out_channels, ho, wo))
+            c, h, w = m.out_channels, ho, wo
+            i += 3
+        elif isinstance(m, nn.Flatten):
+            i += 1
+        else:
+            raise NotImplementedError(f"encoder module {type(m).__name__} not supported by the HIP path")
+    feat = (c, h, w)
+    heads = [vae.mu_c, vae.logvar_c, vae.mu_s, vae.logvar_s]
+    assert heads[0].in_features == c * h * w, "encoder output does not match the latent heads"
+    dec_mods = list(vae.decoder)
+    dec_lin, dec_bn = dec_mods[0], dec_mods[1]
+    assert isinstance(dec_lin, nn.Linear) and isinstance(dec_bn, nn.BatchNorm1d)
+    assert isinstance(dec_mods[2], nn.ReLU) and isinstance(dec_mods[3], nn.Unflatten)
+    unflat = tuple(dec_mods[3].unflattened_size)
+    c, h, w = unflat
+    dec = []
+    i = 4
+    while i < len(dec_mods):
+        m = dec_mods[i]
+        assert isinstance(m, nn.ConvTranspose2d), f"unexpected decoder module {type(m).__name__}"
+        bn = dec_mods[i + 1]
+        act = dec_mods[i + 2]
+        k, s, p, op = m.kernel_size[0], m.stride[0], m.padding[0], m.output_padding[0]
+        ho, wo = _convT_out(h, k, s, p, op), _convT_out(w, k, s, p, op)
+        relu = isinstance(act, nn.ReLU)
+        if not relu:
+            assert isinstance(act, nn.Sigmoid) and i + 3 == len(dec_mods), "Sigmoid must end the decoder"
+        dec.append(ConvSpec(m, bn, relu, True, c, h, w, m.out_channels, ho, wo))
+        c, h, w = m.out_channels, ho, wo
+        i += 3
+    assert (c, h, w) == (in_ch, image_hw, image_hw), "decoder output does not match the input shape"
+    return VaeSpec(in_ch, image_hw, image_hw, vae.z_dim, enc, heads, feat, dec_lin, dec_bn, unflat, dec)
+
+
+# ----------------------------------------------------------------------------- flat parameter arena
+
+
+class ParamArena:
+    """All parameters of a module as views into one flat fp32 buffer (+ a flat gradient buffer)."""
+
+    def __init__(self, params: list, device):
+        self.params = list(params)
+        self.device = torch.device(device)
+        total = sum(p.numel() for p in self.params)
+        self.numel = total
+        self.flat = torch.empty(total, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.offset = {}
+        o = 0
+        with torch.no_grad():
+            for p in self.params:
+                n = p.numel()
+                self.flat[o:o + n].copy_(p.data.reshape(-1).to(self.device, torch.float32))
+                p.data = self.flat[o:o + n].view_as(p)
+                self.offset[id(p)] = (o, n)
+                o += n
+
+    def valid(self) -> bool:
+        base = self.flat.data_ptr()
+        for p in self.params:
+            o, n = self.offset[id(p)]
+            if p.data_ptr() != base + 4 * o or p.device != self.device or p.dtype != torch.float32:
+                return False
+        return True
+
+    def pview(self, p) -> torch.Tensor:
+        o, n = self.offset[id(p)]
+        return self.flat[o:o + n].view_as(p)
+
+    def gview(self, p) -> torch.Tensor:
+        o, n = self.offset[id(p)]
+        return self.grad[o:o + n].view_as(p)
+
+    def gptr(self, p) -> int:
+        return self.grad.data_ptr() + 4 * self.offset[id(p)][0]
+
+    def pptr(self, p) -> int:
+        return self.flat.data_ptr() + 4 * self.offset[id(p)][0]
+
+
+def vae_param_order(vae: nn.Module, spec: VaeSpec) -> list:
+    """Arena order: encoder, the 4 head weights (contiguous [4d, F]), the 4 head biases, decoder."""
+    order = []
+    for c in spec.enc:
+        order += [c.mod.weight, c.mod.bias, c.bn.weight, c.bn.bias]
+    order += [h.weight for h in spec.heads] + [h.bias for h in spec.heads]
+    order += [spec.dec_lin.weight, spec.dec_lin.bias, spec.dec_bn.weight, spec.dec_bn.bias]
+    for c in spec.dec:
+        order += [c.mod.weight, c.mod.bias, c.bn.weight, c.bn.bias]
+    names = {id(p) for p in order}
+    rest = [p for p in vae.parameters() if id(p) not in names]
+    if rest:
+        raise NotImplementedError("VAE has parameters outside the CLEAR-VAE topology")
+    if any(p is None for p in order):
+        raise NotImplementedError("conv/linear layers without bias or BatchNorm without affine")
+    return order
+
+
+def ensure_arena(vae: nn.Module, spec_fn=None):
+    """Attach (or re-attach) a ParamArena + VaeSpec to `vae` on its current device."""
+    arena = getattr(vae, "_cv_arena", None)
+    if arena is not None and arena.valid():
+        return arena
+    spec = vae_spec(vae) if spec_fn is None else spec_fn(vae)
+    dev = next(vae.parameters()).device
+    if dev.type != "cuda":
+        raise RuntimeError(
+            "clear-vae_amd runs on MI355X (ROCm device 'cuda'); move the model with .to('cuda') first"
+        )
+    arena = ParamArena(vae_param_order(vae, spec), dev)
+    vae._cv_arena = arena
+    vae._cv_spec = spec
+    vae._cv_workspaces = {}
+    return arena
+
+
+# ----------------------------------------------------------------------------- BN plumbing
+
+
+class BNView:
+    """One BatchNorm layer: its fp64 stats slots in the workspace and cv_bn builders."""
+
+    def __init__(self, mod: nn.Module, stat: torch.Tensor, gstat: torch.Tensor, count: int):
+        self.mod = mod
+        self.C = mod.num_features
+        self.stat = stat  # [REPL, 2, C] float64
+        self.gstat = gstat
+        self.count = count
+        if mod.momentum is None:
+            raise NotImplementedError("BatchNorm(momentum=None) cumulative averaging is not supported")
+        if not mod.affine or not mod.track_running_stats:
+            raise NotImplementedError("BatchNorm without affine / running stats is not supported")
+
+    def cv(self, train: bool) -> cv_bn:
+        m = self.mod
+        return cv_bn(
+            m.weight.data_ptr(), m.bias.data_ptr(), self.stat.data_ptr(), self.gstat.data_ptr(),
+            m.running_mean.data_ptr(), m.running_var.data_ptr(), self.C, self.count, int(train), float(m.eps),
+        )
+
+
+def operand(x, xf=XF_NONE, bn: cv_bn | None = None, y=None, nchw=0) -> cv_operand:
+    o = cv_operand()
+    o.x = x.data_ptr() if isinstance(x, torch.Tensor) else x
+    o.y = (y.data_ptr() if isinstance(y, torch.Tensor) else y) if y is not None else None
+    o.xf = xf
+    o.nchw = nchw
+    if bn is not None:
+        o.bn = bn
+    return o
+
+
+def ep_none() -> cv_epilogue:
+    e = cv_epilogue()
+    e.stat_mode = STAT_NONE
+    e.stat_div = 1
+    return e
+
+
+def ep_fwd(bnv: BNView) -> cv_epilogue:
+    e = ep_none()
+    e.stat_mode = STAT_FWD
+    e.stat_out = bnv.stat.data_ptr()
+    return e
+
+
+def ep_bwd(bnv: BNView, ey: torch.Tensor, relu: bool, stat_div: int = 1) -> cv_epilogue:
+    e = ep_none()
+    e.stat_mode = STAT_BWD
+    e.stat_out = bnv.gstat.data_ptr()
+    e.stat_div = stat_div
+    e.ey = ey.data_ptr()
+    e.ebn = bnv.cv(True)
+    e.erelu = int(relu)
+    return e
+
+
+# ----------------------------------------------------------------------------- programs
+
+
+class Program:
+    """A fixed list of C-ABI calls (the stream is supplied at run time)."""
+
+    def __init__(self):
+        self.calls = []
+        self.keep = []  # keep ctypes structs alive
+
+    def add(self, name: str, *args):
+        fn = getattr(_lib.lib(), name)
+        conv = []
+        for a in args:
+            if isinstance(a, ctypes.Structure):
+                self.keep.append(a)
+                conv.append(ctypes.byref(a))
+            elif isinstance(a, torch.Tensor):
+                conv.append(a.data_ptr())
+            else:
+                conv.append(a)
+        self.calls.append((name, fn, conv))
+
+    def extend(self, other: "Program"):
+        self.calls += other.calls
+        self.keep += other.keep
+
+    def run(self, stream: int | None = None):
+        s = _lib.stream_handle() if stream is None else stream
+        for name, fn, args in self.calls:
+            rc = fn(*args, s)
+            if rc != 0:
+                _lib.check(rc, name)
+
+
+def struct_array(ctype, items):
+    arr = (ctype * len(items))(*items)
+    return arr
+
+
+def ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+# ----------------------------------------------------------------------------- workspace
+
+
+class Workspace:
+    """Device buffers of one batch size for one model (all NHWC fp32 unless noted)."""
+
+    def __init__(self, spec: VaeSpec, n: int, device, with_grad: bool = True):
+        self.spec, self.n, self.device = spec, n, device
+        f32 = dict(dtype=torch.float32, device=device)
+        d = spec.d
+        self.y_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]
+        self.heads = torch.empty(n, 4 * d, **f32)
+        self.z = torch.empty(n, 2 * d, **f32)
+        self.h = torch.empty(n, spec.dec_lin.out_features, **f32)
+        self.ah = torch.empty(n, spec.dec_lin.out_features, **f32)
+        self.y_dec = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.dec]
+        self.xhat = torch.empty(n, spec.in_ch, spec.H, spec.W, **f32)
+        # fp64 statistics arena: per BN layer [REPL,2,C] forward + [REPL,2,C] backward, plus scalars
+        bns = spec.bn_layers
+        counts = [n * c.h_out * c.w_out for c in spec.enc] + [n] + [n * c.h_out * c.w_out for c in spec.dec]
+        tot = sum(2 * STAT_REPL * 2 * b.num_features for b in bns) + 16
+        self.stats = torch.zeros(tot, dtype=torch.float64, device=device)
+        self.bnv = []
+        o = 0
+        for b, cnt in zip(bns, counts):
+            sz = STAT_REPL * 2 * b.num_features
+            st = self.stats[o:o + sz].view(STAT_REPL, 2, b.num_features)
+            gs = self.stats[o + sz:o + 2 * sz].view(STAT_REPL, 2, b.num_features)
+            self.bnv.append(BNView(b, st, gs, cnt))
+            o += 2 * sz
+        self.scal = self.stats[o:o + 16]  # [0] rec sum, [1] mse work
+        self.bn_enc = self.bnv[: len(spec.enc)]
+        self.bn_1d = self.bnv[len(spec.enc)]
+        self.bn_dec = self.bnv[len(spec.enc) + 1:]
+        if with_grad:
+            self.g_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]
+            self.dheads = torch.empty(n, 4 * d, **f32)
+            self.dz = torch.zeros(n, 2 * d, **f32)
+            self.gah = torch.empty(n, spec.dec_lin.out_features, **f32)
+            self.g_dec = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.dec]
+            self.lse = torch.empty(2, 2 * n, **f32)  # contrastive row log-sum-exps (2 branches)
+            self.losses = torch.zeros(8, **f32)
+            self.mi_work = torch.zeros(int(_lib.lib().cv_mi_workspace_bytes(n)) // 4 + 16, **f32)
+
+    # -- programs --------------------------------------------------------------------------
+    def forward_program(self, x: torch.Tensor, train: bool, eps=None, seed: int = 0, offset=None,
+                        output: str = "xhat", rec_scale=None) -> Program:
+        """Encoder + heads + reparam + decoder (+ running statistics).  output: 'xhat'
+        (cv_output_forward), 'loss' (cv_output_loss with backward seed), 'none' (statistics only)."""
+        P = Program()
+        if train:
+            P.add("cv_zero", self.stats, self.stats.numel() * 8)
+        self.encoder_program(P, x, train)
+        self.reparam_program(P, eps, seed, offset)
+        self.decoder_program(P, self.z, train, output, x, rec_scale)
+        if train:
+            self.running_program(P, "all")
+        return P
+
+    def encoder_program(self, P: Program, x, train: bool):
+        sp, n = self.spec, self.n
+        cur = None
+        for li, c in enumerate(sp.enc):
+            g = c.geom(n)
+            if li == 0:
+                op = operand(x, nchw=1)
+            else:
+                op = operand(cur, XF_BNRELU, self.bn_enc[li - 1].cv(train))
+            ep = ep_fwd(self.bn_enc[li]) if train else ep_none()
+            P.add("cv_conv_forward", g, op, c.mod.weight, c.mod.bias, self.y_enc[li], ep)
+            cur = self.y_enc[li]
+        # heads (Linear on the NCHW-flattened activation), split-K into a zeroed buffer
+        C, Hh, Wh = sp.feat
+        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
+        P.add("cv_zero", self.heads, self.heads.numel() * 4)
+        P.add("cv_linear_forward", lin, operand(cur, XF_BNRELU, self.bn_enc[-1].cv(train)),
+              sp.heads[0].weight.data_ptr(), sp.heads[0].bias.data_ptr(), self.heads, 1, ep_none())
+
+    def reparam_program(self, P: Program, eps=None, seed: int = 0, offset=None):
+        P.add("cv_reparam_forward", self.heads, self.n, self.spec.d, eps.data_ptr() if eps is not None else None,
+              ctypes.c_uint64(seed), offset.data_ptr() if offset is not None else None, self.z, None)
+
+    def running_program(self, P: Program, which: str = "all"):
+        views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
+        bns = struct_array(cv_bn, [b.cv(True) for b in views])
+        nbt = ptr_array([b.mod.num_batches_tracked.data_ptr() for b in views])
+        P.add("cv_bn_update_running", bns, len(views), ctypes.c_float(float(views[0].mod.momentum)), nbt)
+
+    def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None):
+        sp, n = self.spec, self.n
+        Cu, Hu, Wu = sp.unflat
+        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
+        ep = ep_fwd(self.bn_1d) if train else ep_none()
+        P.add("cv_linear_forward", lin, operand(z), sp.dec_lin.weight, sp.dec_lin.bias, self.h, 0, ep)
+        P.add("cv_bn_apply", self.bn_1d.cv(train), self.h, self.ah, n, sp.dec_lin.out_features, Hu * Wu, Cu, 1)
+        cur = self.ah
+        for li, c in enumerate(sp.dec):
+            g = c.geom(n)
+            op = operand(cur) if li == 0 else operand(cur, XF_BNRELU, self.bn_dec[li - 1].cv(train))
+            ep = ep_fwd(self.bn_dec[li]) if train else ep_none()
+            P.add("cv_conv_forward", g, op, c.mod.weight, c.mod.bias, self.y_dec[li], ep)
+            cur = self.y_dec[li]
+        last = sp.dec[-1]
+        hw = last.h_out * last.w_out
+        if output == "xhat":
+            P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)
+        elif output == "loss":
+            assert train
+            P.add("cv_output_loss", self.bn_dec[-1].cv(True), cur, x, n, sp.in_ch, hw, self.xhat,
+                  self.scal[0:1], self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
+
+    def decoder_backward_program(self, P: Program, param_grad, dz_out):
+        """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to
+        dz_out [n, 2d] (zeroed + accumulated) and the decoder parameter gradients."""
+        sp, n = self.spec, self.n
+        L = len(sp.dec)
+        for li in range(L - 1, -1, -1):
+            c = sp.dec[li]
+            g = c.geom(n)
+            gout = operand(self.g_dec[li], XF_BNBWD, self.bn_dec[li].cv(True), y=self.y_dec[li])
+            if li > 0:
+                ep = ep_bwd(self.bn_dec[li - 1], self.y_dec[li - 1], sp.dec[li - 1].relu)
+                P.add("cv_conv_backward_data", g, gout, c.mod.weight, self.g_dec[li - 1], ep)
+                xin = operand(self.y_dec[li - 1], XF_BNRELU, self.bn_dec[li - 1].cv(True))
+            else:
+                P.add("cv_conv_backward_data", g, gout, c.mod.weight, self.gah, ep_none())
+                xin = operand(self.ah)
+            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0)
+        Cu, Hu, Wu = sp.unflat
+        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
+        P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
+              self.z, param_grad(sp.dec_lin.weight))
+        P.add("cv_zero", dz_out, dz_out.numel() * 4)
+        gout = operand(self.gah, XF_BNBWD, self.bn_1d.cv(True), y=self.h)
+        P.add("cv_linear_backward_data", lin, gout, sp.dec_lin.weight, dz_out, 1, ep_none())
+
+    def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None):
+        """From d(heads) [n, 4d] to the encoder / heads parameter gradients (and dx if asked)."""
+        sp, n = self.spec, self.n
+        C, Hh, Wh = sp.feat
+        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
+        a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
+        P.add("cv_linear_backward_weight", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
+              param_grad(sp.heads[0].bias), 0)
+        ep = ep_bwd(self.bn_enc[-1], self.y_enc[-1], True, stat_div=Hh * Wh)
+        P.add("cv_linear_backward_data", lin, operand(dheads), sp.heads[0].weight, self.g_enc[-1], 0, ep)
+        for li in range(len(sp.enc) - 1, -1, -1):
+            c = sp.enc[li]
+            g = c.geom(n)
+            gout = operand(self.g_enc[li], XF_BNBWD, self.bn_enc[li].cv(True), y=self.y_enc[li])
+            if li > 0:
+                ep = ep_bwd(self.bn_enc[li - 1], self.y_enc[li - 1], True)
+                P.add("cv_conv_backward_data", g, gout, c.mod.weight, self.g_enc[li - 1], ep)
+                xin = operand(self.y_enc[li - 1], XF_BNRELU, self.bn_enc[li - 1].cv(True))
+            else:
+                if dx is not None:
+                    P.add("cv_conv_backward_data", g, gout, c.mod.weight, dx, ep_none())
+                xin = operand(x, nchw=1)
+            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0)
+
+    def bn_grads_program(self, P: Program, param_grad, which: str = "all"):
+        views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
+        bns = struct_array(cv_bn, [b.cv(True) for b in views])
+        dg = ptr_array([param_grad(b.mod.weight) for b in views])
+        db = ptr_array([param_grad(b.mod.bias) for b in views])
+        P.add("cv_bn_param_grads", bns, len(views), dg, db)

@@ -1,0 +1,157 @@
+"""Loss functions with the reference's names and signatures (code/src/losses.py).
+
+Hot path — HIP kernels through cvhip.autograd:
+  vae_loss           -> cv_mse_sum + cv_kl          (losses.py:36-50)
+  contrastive_loss   -> cv_ntxent, all five sims    (losses.py:98-137)
+The pairwise_* / snn_loss / logsumexp helpers keep the reference's tensor-level semantics for
+callers that use them directly (they are building blocks, not the trained path); the supcon / lam
+losses and the sklearn metrics are outside the hot path and stay as in the
+reference (sklearn on CPU).
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from sklearn.feature_selection import mutual_info_classif
+from sklearn.metrics import average_precision_score, roc_auc_score
+from torch import Tensor
+
+from cvhip import autograd as _ag
+from cvhip._lib import SIM
+
+# ----------------------------------------------------------------------------- metrics (CPU)
+
+
+def mutual_info_gap(label, latent_c, latent_s):
+    """gMIG (losses.py:10-16): sklearn kNN MI on the CPU, as in the reference."""
+    label, latent_c, latent_s = label.cpu(), latent_c.cpu(), latent_s.cpu()
+    p = torch.bincount(label) / len(label)
+    H = float(-(p * torch.log(p)).sum())
+    mi_c = mutual_info_classif(latent_c, label, discrete_features=False)
+    mi_s = mutual_info_classif(latent_s, label, discrete_features=False)
+    return (mi_c.mean() - mi_s.mean()) / H
+
+
+def accurary(logit: torch.Tensor, y: torch.Tensor):
+    yh = logit.argmax(dim=1).cpu()
+    return (yh.view(-1) == y.view(-1)).float().mean()
+
+
+def auc(logit: torch.Tensor, y: torch.Tensor):
+    num_classes = int(y.max() + 1)
+    ph = logit.softmax(dim=1).detach().cpu()
+    y = y.cpu()
+    yb = torch.eye(num_classes)[y]
+    aupr, auroc = dict(), dict()
+    for i in range(num_classes):
+        aupr[i] = round(average_precision_score(yb[:, i], ph[:, i]), 3)
+        auroc[i] = round(roc_auc_score(yb[:, i], ph[:, i]), 3)
+    return aupr, auroc
+
+
+# ----------------------------------------------------------------------------- ELBO
+
+
+def sample_level_reduction(tensor: Tensor):
+    """sum over every non-batch dim, mean over the batch (losses.py:36-38)."""
+    return tensor.sum(dim=list(range(len(tensor.shape)))[1:]).mean()
+
+
+def vae_loss(x_reconstr, x, mu_c, mu_s, logvar_c, logvar_s):
+    """(reconstruction, kl_c, kl_s) of losses.py:41-50 on the device."""
+    _ag._require_gpu(x_reconstr, x, mu_c, mu_s, logvar_c, logvar_s)
+    return _ag.VaeLossFn.apply(x_reconstr, x, mu_c, mu_s, logvar_c, logvar_s)
+
+
+# ----------------------------------------------------------------------------- pairwise similarities
+
+
+def pairwise_cosine(mu: torch.Tensor):
+    return F.cosine_similarity(mu[None, :, :], mu[:, None, :], dim=-1)
+
+
+def pairwise_l2(mu: torch.Tensor):
+    return -((mu[None, :, :] - mu[:, None, :]) ** 2).sum(dim=-1)
+
+
+def pairwise_jeffrey_div(mu: torch.Tensor, logvar: torch.Tensor):
+    k = mu.shape[1]
+    var = logvar.exp()
+    t1 = logvar.sum(dim=-1)[None, :] - logvar.sum(dim=-1)[:, None] - k
+    t2 = ((mu[None, :, :] - mu[:, None, :]) ** 2 / var).sum(dim=-1)
+    t3 = (var[None, :, :] / (var[:, None, :] + 1e-8)).sum(dim=-1)
+    kl = 0.5 * (t1 + t2 + t3)
+    return -(0.5 * (kl + kl.T))
+
+
+def pairwise_mahalanobis_dis(mu: torch.Tensor, logvar: torch.Tensor):
+    var = 0.5 * (logvar.exp()[None, :, :] + logvar.exp()[:, None, :])
+    return -((mu[None, :, :] - mu[:, None, :]) ** 2 / var).sum(dim=-1)
+
+
+def pairwise_modified_l2_dis(mu: torch.Tensor, logvar: torch.Tensor):
+    var = (0.5 * (logvar[None, :, :] + logvar[:, None, :])).exp()
+    return -((mu[None, :, :] - mu[:, None, :]) ** 2 / var).sum(dim=-1)
+
+
+def logsumexp(x: Tensor, dim: int) -> Tensor:
+    """Stable logsumexp where an all -inf slice gives -inf (losses.py:87-95)."""
+    m, _ = x.max(dim=dim)
+    mask = m == -float("inf")
+    s = (x - m.masked_fill(mask, 0).unsqueeze(dim=dim)).exp().sum(dim=dim)
+    return s.masked_fill(mask, 1).log() + m.masked_fill(mask, -float("inf"))
+
+
+# ----------------------------------------------------------------------------- contrastive
+
+
+def contrastive_loss(mu: torch.Tensor, logvar: torch.Tensor, label: torch.Tensor, sim_fn: str,
+                     temperature: float, loss_name: str = "snn_loss", ps: bool = False):
+    """SNN contrastive loss of losses.py:98-126 as one fused HIP op (cv_ntxent): similarity, label
+    masks, masked log-sum-exps and the mean over finite rows, with its analytic backward."""
+    if sim_fn not in SIM:
+        raise ValueError("unimplemented similarity measure.")
+    if loss_name != "snn_loss":
+        # the reference's only trained loss; supcon variants are defined but never called
+        raise NotImplementedError(f"{loss_name} is not on the HIP path (only snn_loss)")
+    _ag._require_gpu(mu, logvar, label)
+    return _ag.ContrastiveFn.apply(mu, logvar, label, sim_fn, temperature, bool(ps))
+
+
+def snn_loss(sim: torch.Tensor, pair_mat: torch.Tensor, temperature: float):
+    """Row losses from a similarity matrix (losses.py:129-137); fills the diagonal in place like the
+    reference."""
+    n = sim.shape[0]
+    sim[torch.eye(n, device=sim.device).bool()] = float("-Inf")
+    neg_mask = pair_mat == 0
+    pos = pair_mat * sim
+    pos[neg_mask] = float("-Inf")
+    return -logsumexp(pos / temperature, dim=1) + logsumexp(sim / temperature, dim=1)
+
+
+def supcon_in_loss(sim: torch.Tensor, pair_mat: torch.Tensor, temperature: float):
+    n_k = pair_mat.sum(dim=1) - 1
+    n = sim.shape[0]
+    sim[torch.eye(n, device=sim.device).bool()] = float("-Inf")
+    neg_mask = pair_mat == 0
+    pos = pair_mat * sim
+    pos[neg_mask] = float("-Inf")
+    return n_k.log() - logsumexp(pos / temperature, dim=1) + logsumexp(sim / temperature, dim=1)
+
+
+def supcon_out_loss(sim: torch.Tensor, pair_mat: torch.Tensor, temperature: float):
+    n = sim.shape[0]
+    sim[torch.eye(n, device=sim.device).bool()] = -999
+    pos_mask = pair_mat * (1 - torch.eye(n)).to(sim.device)
+    masked = sim * pos_mask
+    n_k = pos_mask.sum(dim=1)
+    select = n_k > 0
+    return -masked.sum(dim=1)[select] / n_k[select] + logsumexp(sim[select] / temperature, dim=1)
+
+
+def lam_loss(feature_x: torch.Tensor, feature_x_tilde: torch.Tensor, y: torch.Tensor,
+             linear_w: torch.nn.Parameter):
+    """Labelled LAM (losses.py:173-187), CNN baseline only."""
+    w_y = linear_w[y]
+    return ((feature_x * w_y - feature_x_tilde * w_y) ** 2).sum(dim=1).mean()

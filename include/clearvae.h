@@ -1,0 +1,270 @@
+/*
+ * clearvae.h — C-ABI of libclearvae_hip.so, the MI355X (gfx950) hot path of CLEAR-VAE training.
+ *
+ * The reference (scotsun/clear-vae) is pure PyTorch eager and has no FFI; every entry point below
+ * replaces a group of ATen calls made by the reference's Python code.  Each declaration cites the
+ * reference lines (paths relative to the reference's repo root) whose arithmetic it implements.
+ * The Python binding is clear-vae_amd/cvhip/_lib.py (ctypes); see INTEGRATION.md.
+ *
+ * Conventions
+ *   - every pointer is a device pointer owned by the caller (PyTorch's caching allocator); the library
+ *     never allocates, frees or synchronises, so every call can be captured into a HIP graph;
+ *   - activations are NHWC fp32 ("pixels x channels" row-major); weights keep PyTorch's layouts
+ *     (Conv2d [Cout][Cin][kh][kw], ConvTranspose2d [Cin][Cout][kh][kw], Linear [out][in]);
+ *   - BatchNorm batch statistics are accumulated in fp64 by the producing kernel's epilogue into
+ *     CV_STAT_REPL replicas of [2][C] doubles (sum, sum of squares / sum dz, sum dz*xhat) and folded
+ *     into per-channel constants by the consuming kernel's prologue (the normalised activation is
+ *     never written to HBM);
+ *   - return value 0 = success; otherwise cv_last_error() describes the failure (host-side checks
+ *     run before any launch, so a failing call enqueues nothing).
+ */
+#ifndef CLEARVAE_H
+#define CLEARVAE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* cv_stream_t; /* a hipStream_t (torch.cuda.current_stream().cuda_stream) */
+
+#define CV_STAT_REPL 8
+
+/* ---- BatchNorm as seen by a fused prologue/epilogue (nn.BatchNorm1d/2d, vae.py:17-44, 115-154) ---- */
+typedef struct cv_bn {
+  const float* gamma;        /* [C] PyTorch order                                              */
+  const float* beta;         /* [C]                                                            */
+  const double* stat;        /* [REPL][2][C] forward sums (sum x, sum x^2) of the layer input  */
+  const double* gstat;       /* [REPL][2][C] backward sums (sum dz, sum dz*xhat)               */
+  const float* running_mean; /* [C]                                                            */
+  const float* running_var;  /* [C]                                                            */
+  int C;                     /* normalised features                                            */
+  int count;                 /* elements per feature in the batch (N*H*W, or N for BN1d)       */
+  int train;                 /* 1: batch statistics, 0: running statistics (eval mode)         */
+  float eps;
+} cv_bn;
+
+/* transform applied while an operand is staged into LDS */
+enum { CV_XF_NONE = 0, CV_XF_BNRELU = 1, CV_XF_BNBWD = 2 };
+/*   CV_XF_BNRELU : v = max(x*gamma*istd + (beta - mean*gamma*istd), 0)               (BN fwd + ReLU)
+ *   CV_XF_BNBWD  : v = gamma*istd*(dz - sum(dz)/n - xhat*sum(dz*xhat)/n), xhat from y  (BN bwd)      */
+
+typedef struct cv_operand {
+  const float* x;  /* primary tensor: activation, or dz (masked upstream gradient) for BNBWD    */
+  const float* y;  /* BNBWD only: the BN layer's input (pre-BN values), same layout as x        */
+  int xf;          /* CV_XF_*                                                                  */
+  int nchw;        /* 1: x is NCHW (network input, channels not a multiple of 4); else NHWC    */
+  cv_bn bn;        /* constants source for the transform                                       */
+} cv_operand;
+
+/* epilogue statistics of the produced tensor */
+enum { CV_STAT_NONE = 0, CV_STAT_FWD = 1, CV_STAT_BWD = 2 };
+/*   CV_STAT_FWD: out is the input of a BN layer; accumulate (sum v, sum v^2) into stat_out.
+ *   CV_STAT_BWD: out is d(post-ReLU activation) of BN layer `ebn` whose input is `ey`; the kernel
+ *                stores dz = v * [relu active] and accumulates (sum dz, sum dz*xhat) into stat_out. */
+
+typedef struct cv_epilogue {
+  int stat_mode;      /* CV_STAT_*                                                  */
+  double* stat_out;   /* [REPL][2][C]                                               */
+  int stat_div;       /* feature index = column / stat_div (1 = per column)         */
+  const float* ey;    /* STAT_BWD: pre-BN values at the output positions            */
+  cv_bn ebn;          /* STAT_BWD: the BN layer (batch statistics)                  */
+  int erelu;          /* STAT_BWD: 1 if ReLU follows that BN                        */
+} cv_epilogue;
+
+/* ---- convolution geometry (nn.Conv2d / nn.ConvTranspose2d, vae.py:15-46, 113-156) ---- */
+typedef struct cv_conv {
+  int n;                          /* batch                                         */
+  int c_in, h_in, w_in;           /* layer input  (NHWC)                           */
+  int c_out, h_out, w_out;        /* layer output (NHWC)                           */
+  int kh, kw, stride, pad;
+  int transposed;                 /* 0 Conv2d, 1 ConvTranspose2d                   */
+} cv_conv;
+
+/* y = conv(T(x)) + bias.  Replaces nn.Conv2d/ConvTranspose2d.forward (vae.py:15-46) with the
+ * preceding BatchNorm2d+ReLU fused into the operand load and the following BatchNorm2d's batch
+ * statistics fused into the epilogue. */
+int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* weight, const float* bias,
+                    float* out, const cv_epilogue* ep, cv_stream_t stream);
+
+/* dx = conv^T(T(dy)).  Replaces the grad_input half of aten::convolution_backward. */
+int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* weight,
+                          float* gin, const cv_epilogue* ep, cv_stream_t stream);
+
+/* dw += sum_pixels T(x) (x) T(dy).  Replaces the grad_weight half of aten::convolution_backward.
+ * split_k <= 0 picks a split; gweight (and gbias) must be zeroed by the caller (atomic
+ * accumulation).  gbias (optional, Conv2d only) += sum_pixels T(dy). */
+int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, const cv_operand* gout,
+                            float* gweight, float* gbias, int split_k, cv_stream_t stream);
+
+/* ---- fully connected layers (nn.Linear heads vae.py:27-30; decoder Linear vae.py:33) ----
+ * A linear layer whose input (or output) is the NCHW-flattened view of an NHWC activation with
+ * `*_pix` pixels and `*_ch` channels (nn.Flatten vae.py:25 / nn.Unflatten vae.py:36).              */
+typedef struct cv_linear {
+  int n;               /* batch rows                         */
+  int in_features, out_features;
+  int in_pix, in_ch;   /* in_features = in_pix*in_ch, or in_pix = 1 for a plain row-major input   */
+  int out_pix, out_ch; /* same for the output                                                      */
+} cv_linear;
+
+int cv_linear_forward(const cv_linear* g, const cv_operand* in, const float* weight,
+                      const float* bias, float* out, int accumulate, const cv_epilogue* ep,
+                      cv_stream_t stream);
+int cv_linear_backward_data(const cv_linear* g, const cv_operand* gout, const float* weight,
+                            float* gin, int accumulate, const cv_epilogue* ep, cv_stream_t stream);
+int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
+                              float* gweight, float* gbias, int split_k, cv_stream_t stream);
+
+/* Decoder Linear -> BatchNorm1d -> ReLU backward (vae.py:33-35).  da: gradient w.r.t. the ReLU
+ * output in the Unflatten/NHWC order (g->out_pix, g->out_ch); h: the Linear output (BN1d input),
+ * same order.  The kernel masks da in place (da <- dz), writes the BN1d backward sums into
+ * gstat_out (replica 0; other replicas must be zero) and the Linear weight gradient
+ * dW[f][k] = sum_n BNbwd(dz)[n][f] * zin[n][k] (overwrite, no accumulation). */
+int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, const cv_bn* bn,
+                                 double* gstat_out, const float* zin, float* gweight,
+                                 cv_stream_t stream);
+
+/* out = max(BN(x), 0) elementwise for a BatchNorm1d over `features` PyTorch-order features whose
+ * tensor is stored in the Unflatten/NHWC order (pix, ch) (vae.py:34-36); rows = batch. */
+int cv_bn_apply(const cv_bn* bn, const float* x, float* out, int rows, int features, int pix, int ch,
+                int relu, cv_stream_t stream);
+
+/* ---- BatchNorm running statistics (nn.BatchNorm*, momentum 0.1, unbiased running var) ---- */
+int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum,
+                         int64_t* const* num_batches_tracked, cv_stream_t stream);
+/* copy batch stats into (mean, invstd) float arrays (for tests / PyTorch-visible save_mean) */
+int cv_bn_batch_stats(const cv_bn* bn, float* mean, float* invstd, cv_stream_t stream);
+
+/* ---- decoder output: BatchNorm2d(C) + Sigmoid (vae.py:44-45) ---- */
+/* xhat = sigmoid(BN(y)), written NCHW [n][c][h][w]; y is NHWC [n][h][w][c]. */
+int cv_output_forward(const cv_bn* bn, const float* y, int n, int c, int hw, float* xhat,
+                      cv_stream_t stream);
+/* fused output + reconstruction loss (losses.py:36-47): rec = mean_n sum_chw (xhat - x)^2 into
+ * rec_out[0] (fp64 accumulate; caller zeroes), and when dv_out != NULL the gradient of
+ * (rec_scale*rec) w.r.t. the BN output: dv = rec_scale*2(xhat-x)/n * xhat(1-xhat) (NHWC), plus the
+ * BN backward sums into gstat_out.  rec_scale may be NULL (1.0). x is NCHW. */
+int cv_output_loss(const cv_bn* bn, const float* y, const float* x, int n, int c, int hw,
+                   float* xhat, double* rec_out, float* dv_out, double* gstat_out,
+                   const float* rec_scale, cv_stream_t stream);
+/* backward of xhat = sigmoid(BN(y)) given dxhat (NCHW): dv (NHWC) + BN backward sums. */
+int cv_output_backward(const cv_bn* bn, const float* y, const float* xhat, const float* dxhat,
+                       int n, int c, int hw, float* dv_out, double* gstat_out, cv_stream_t stream);
+
+/* ---- reparameterisation (vae.py:56-79) ---- */
+/* heads: [n][4d] = (mu_c | logvar_c | mu_s | logvar_s); z: [n][2d] = (z_c | z_s).
+ * eps == NULL: eps ~ N(0,1) from a counter-based Philox4x32-10 stream keyed by (seed, offset[0]);
+ * offset is a device uint64 advanced by the kernel (graph-replay safe).  eps != NULL: [n][2d]
+ * injected noise (test hook).  eps_out (optional) receives the noise used. */
+int cv_reparam_forward(const float* heads, int n, int d, const float* eps, uint64_t seed,
+                       uint64_t* offset, float* z, float* eps_out, cv_stream_t stream);
+
+/* VAE.sample for one factor (vae.py:56-60): z = mu + eps*exp(0.5*logvar), [n][d] contiguous;
+ * eps injected or drawn from Philox(seed, offset[0]) (offset advanced).  Backward:
+ * dmu = dz, dlogvar = dz*(z-mu)/2 (accumulated into dmu/dlogvar when accumulate != 0). */
+int cv_sample_forward(const float* mu, const float* logvar, long numel, const float* eps,
+                      uint64_t seed, uint64_t* offset, float* z, cv_stream_t stream);
+int cv_sample_backward(const float* mu, const float* z, const float* dz, long numel, float* dmu,
+                       float* dlogvar, int accumulate, cv_stream_t stream);
+
+/* ---- latent-space losses (losses.py:41-137) ---- */
+enum { CV_SIM_COSINE = 0, CV_SIM_L2 = 1, CV_SIM_MODIFIED_L2 = 2, CV_SIM_JEFFREY = 3,
+       CV_SIM_MAHALANOBIS = 4 };
+
+/* KL term of vae_loss (losses.py:48-49): kl = -0.5 * mean_n sum_d(1 + lv - mu^2 - exp(lv));
+ * with dmu/dlogvar != NULL also writes (or accumulates) gscale[0] * d kl / d(mu, logvar). */
+int cv_kl(const float* mu, const float* logvar, int ld, int n, int d, float* kl_out,
+          const float* gscale, float* dmu, float* dlogvar, int gld, int accumulate,
+          cv_stream_t stream);
+
+/* Fused-step seed of d(heads): KL(c), KL(s) with the LogisticAnnealer weight
+ * w = beta/(1+exp(-(t-loc)/scale)), t = anneal_step[0] (trainer.py:22-38, 474-477), plus the decoder
+ * gradient dz chained through z = mu + eps*exp(lv/2).  losses[0] = rec_in[0] (if given),
+ * losses[1], losses[2] = kl_c, kl_s; losses[7] = w.  dheads is overwritten. */
+int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
+                      float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                      float* dheads, float* losses, cv_stream_t stream);
+
+/* reconstruction term (losses.py:45-47) for the autograd path: rec = mean_n sum (xhat - x)^2;
+ * work: one zeroed fp64 word.  dxhat != NULL: dxhat = gscale[0] * 2 (xhat - x) / n. */
+int cv_mse_sum(const float* xhat, const float* x, int n, int per_sample, float* rec_out,
+               const float* gscale, float* dxhat, double* work, cv_stream_t stream);
+
+/* SNN / NT-Xent contrastive loss (losses.py:98-137) for up to 2 branches sharing labels
+ * (content: pairs with equal labels; style with ps=1: pairs with different labels,
+ * trainer.py:456-472).  phase 0: row log-sum-exps into lse; phase 1: loss (mean over finite rows,
+ * losses.py:125-126) and, when dmu != NULL, the gradient gmul*gscale[0]*dloss/d(mu, logvar);
+ * phase 2: both. */
+typedef struct cv_ntxent_branch {
+  const float* mu; const float* logvar; int ld;   /* [n] rows of stride ld               */
+  int ps;
+  float* dmu; float* dlogvar; int gld;            /* gradient outputs (may be NULL)       */
+  const float* gscale; float gmul;                /* upstream gradient                    */
+  float* loss_out;                                /* [1]                                  */
+  float* lse;                                     /* workspace [2n]                       */
+} cv_ntxent_branch;
+int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
+              float temperature, int phase, int accumulate, cv_stream_t stream);
+
+/* ---- MI upper bounds (mi_estimator.py:108-198) ---- */
+enum { CV_MI_NONE = 0, CV_MI_CLUBSAMPLE = 1, CV_MI_L1OUT = 2 };
+
+/* q(y|x) MLPs (mi_estimator.py:111-122): p_mu = L(dx,h)-ReLU-L(h,dy);
+ * p_logvar = L(dx,h)-ReLU-L(h,dy)-Tanh; Linear weights [out][in]; h = hidden_size // 2. */
+typedef struct cv_mlp {
+  const float *w1, *b1, *w2, *b2;   /* p_mu     */
+  const float *w3, *b3, *w4, *b4;   /* p_logvar */
+  int dx, h, dy;
+} cv_mlp;
+typedef struct cv_mlp_grad {
+  float *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4;
+} cv_mlp_grad;
+
+size_t cv_mi_workspace_bytes(int n);
+/* CLUBSample.forward (mi_estimator.py:133-143; perm injected, or generated on device from
+ * (seed, offset)) and L1OutUB.forward (mi_estimator.py:170-191, with the reference's [N,N,N]
+ * broadcasting reduced to its O(N d) closed form).  Writes mi_out[0]; leaves perm / column sums
+ * in `work` for cv_mi_backward. */
+int cv_mi_forward(int kind, const cv_mlp* mlp, const float* x, int ldx, const float* y, int ldy,
+                  int n, const int64_t* perm, uint64_t seed, uint64_t* offset, void* work,
+                  float* mi_out, cv_stream_t stream);
+/* gradient of gmul*gscale[0]*mi w.r.t. x and y (written or accumulated) and, when g != NULL, the MLP
+ * parameters (accumulated).  Chain mode (dheads != NULL): x = z_c, y = z_s are the two halves of z
+ * and the gradient is accumulated into d(heads) through z = mu + eps*exp(lv/2). */
+int cv_mi_backward(int kind, const cv_mlp* mlp, const float* x, int ldx, const float* y, int ldy,
+                   int n, void* work, const float* gscale, float gmul, float* dx, float* dy,
+                   int gld, int accumulate, const cv_mlp_grad* g, const float* heads,
+                   const float* z, float* dheads, int d, cv_stream_t stream);
+/* learning_loss = -loglikeli (mi_estimator.py:129-131, 193-198): loss and MLP gradients
+ * (overwritten); with params != NULL also the Adam update of the estimator arena
+ * (trainer.py:885-887). */
+int cv_mi_learning_step(const cv_mlp* mlp, const float* x, int ldx, const float* y, int ldy, int n,
+                        float* loss_out, const cv_mlp_grad* g, float* params, const float* grads,
+                        float* exp_avg, float* exp_avg_sq, int64_t numel, const float* hyper,
+                        int64_t* step, cv_stream_t stream);
+
+/* ---- Adam (torch.optim.Adam foreach semantics) over a flat fp32 arena ----
+ * hyper: device float[8] = lr, beta1, beta2, eps, weight_decay; step: device int64[2] =
+ * (steps taken, arrival counter = 0).  grad_scale (device float or NULL) multiplies the gradient
+ * first (data-parallel averaging); aux_counter (or NULL) is incremented once per call
+ * (LogisticAnnealer.step, trainer.py:484). */
+int cv_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                 int64_t numel, const float* hyper, int64_t* step, const float* grad_scale,
+                 int64_t* aux_counter, cv_stream_t stream);
+
+/* BatchNorm affine gradients from the backward sums: dgamma = sum dz*xhat, dbeta = sum dz
+ * (nn.BatchNorm weight/bias grads); written (not accumulated) for up to 16 layers. */
+int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dgamma, float* const* dbeta,
+                      cv_stream_t stream);
+
+/* ---- misc ---- */
+/* hipMemsetAsync(ptr, 0, bytes, stream) (graph-capturable) */
+int cv_zero(void* ptr, size_t bytes, cv_stream_t stream);
+const char* cv_last_error(void);
+int cv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLEARVAE_H */

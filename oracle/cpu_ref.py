@@ -1,0 +1,348 @@
+"""ORACLE — test infrastructure only (never imported by the product path).
+
+A functional, CPU restatement of the reference's CLEAR-VAE hot path (scotsun/clear-vae @ code/src),
+written against torch.nn.functional so that it runs in fp32 or fp64 on the host.  It restates:
+
+  VAE / VAE64 forward          code/src/models/vae.py:15-46, 48-102, 113-156
+  vae_loss                     code/src/losses.py:36-50
+  pairwise similarities        code/src/losses.py:53-84
+  logsumexp / snn_loss         code/src/losses.py:87-95, 129-137
+  contrastive_loss             code/src/losses.py:98-126
+  CLUBSample / L1OutUB         code/src/models/mi_estimator.py:108-198
+  LogisticAnnealer             code/src/trainer.py:22-38
+  CLEARVAETrainer step         code/src/trainer.py:447-484
+  ClearMIMVAETrainer step      code/src/trainer.py:842-888
+with the reparameterisation noise and the CLUB-S permutation passed in explicitly.
+Gradients come from torch autograd on the CPU.
+
+Pinning: tests/golden/*.npz hold outputs of the REAL reference (imported from /root/reference in the
+development container by tests/golden/gen_golden.py, fp64, same deterministic weights / inputs /
+noise); tests/test_oracle_golden.py checks this restatement against them.  Only tests/, the
+__graft_entry__.smoke() check and bench.py's cpu_baseline leg use this module.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+# ----------------------------------------------------------------------------- architecture tables
+# (in, out, k, s, p[, op]); None = image channels.   vae.py:15-46 (VAE) and :113-156 (VAE64)
+ENC = {"VAE": [(None, 32, 3, 2, 1), (32, 64, 3, 2, 1), (64, 128, 3, 2, 1)],
+       "VAE64": [(None, 32, 4, 2, 1), (32, 64, 4, 2, 1), (64, 128, 4, 2, 1), (128, 256, 4, 2, 1),
+                 (256, 512, 4, 2, 1)]}
+DEC = {"VAE": [(128, 64, 3, 2, 1, 0), (64, 32, 3, 2, 1, 1), (32, None, 3, 2, 1, 1)],
+       "VAE64": [(512, 256, 4, 2, 1, 0), (256, 128, 4, 2, 1, 0), (128, 64, 4, 2, 1, 0), (64, 32, 4, 2, 1, 0),
+                 (32, None, 4, 2, 1, 0)]}
+UNFLAT = {"VAE": (128, 4, 4), "VAE64": (512, 2, 2)}
+IMAGE = {"VAE": 28, "VAE64": 64}
+
+
+def state_keys(arch: str, z_total: int, in_ch: int):
+    """state_dict keys/shapes of the reference module tree (parameters and BN buffers)."""
+    d = z_total // 2
+    out = []
+    i = 0
+    for cin, cout, k, s, p in ENC[arch]:
+        cin = in_ch if cin is None else cin
+        out += [(f"encoder.{i}.weight", (cout, cin, k, k)), (f"encoder.{i}.bias", (cout,))]
+        out += [(f"encoder.{i + 1}.{n}", (cout,)) for n in ("weight", "bias", "running_mean", "running_var")]
+        out += [(f"encoder.{i + 1}.num_batches_tracked", ())]
+        i += 3
+    for h in ("mu_c", "logvar_c", "mu_s", "logvar_s"):
+        out += [(f"{h}.weight", (d, 2048)), (f"{h}.bias", (d,))]
+    out += [("decoder.0.weight", (2048, 2 * d)), ("decoder.0.bias", (2048,))]
+    out += [(f"decoder.1.{n}", (2048,)) for n in ("weight", "bias", "running_mean", "running_var")]
+    out += [("decoder.1.num_batches_tracked", ())]
+    i = 4
+    for cin, cout, k, s, p, op in DEC[arch]:
+        cout = in_ch if cout is None else cout
+        out += [(f"decoder.{i}.weight", (cin, cout, k, k)), (f"decoder.{i}.bias", (cout,))]
+        out += [(f"decoder.{i + 1}.{n}", (cout,)) for n in ("weight", "bias", "running_mean", "running_var")]
+        out += [(f"decoder.{i + 1}.num_batches_tracked", ())]
+        i += 3
+    return out
+
+
+def det_state(arch: str, z_total: int, in_ch: int, seed: int = 0) -> dict:
+    """Deterministic, platform-independent weights (numpy PCG64): U(-b, b) with the PyTorch default
+    bound b = 1/sqrt(fan_in) for conv/linear, BN weight U(0.5, 1.5), BN bias U(-0.1, 0.1), running
+    stats at their defaults.  Used by the golden generator AND the tests so no weights are stored."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for name, shape in state_keys(arch, z_total, in_ch):
+        if name.endswith("num_batches_tracked"):
+            sd[name] = np.array(0, dtype=np.int64)
+            continue
+        if name.endswith("running_mean"):
+            sd[name] = np.zeros(shape)
+            continue
+        if name.endswith("running_var"):
+            sd[name] = np.ones(shape)
+            continue
+        parts = name.split(".")
+        is_bn = False
+        if parts[0] in ("encoder", "decoder"):
+            idx = int(parts[1])
+            layer_kind = _layer_kind(arch, parts[0], idx)
+            is_bn = layer_kind == "bn"
+        if is_bn:
+            sd[name] = rng.uniform(0.5, 1.5, shape) if parts[-1] == "weight" else rng.uniform(-0.1, 0.1, shape)
+            continue
+        wname = ".".join(parts[:-1]) + ".weight"
+        wshape = dict(state_keys(arch, z_total, in_ch))[wname]
+        if len(wshape) == 4:
+            is_t = parts[0] == "decoder"
+            fan_in = (wshape[0] if is_t else wshape[1]) * wshape[2] * wshape[3]
+            if is_t:  # ConvTranspose2d fan_in = weight.size(1) * k * k in torch's init
+                fan_in = wshape[1] * wshape[2] * wshape[3]
+        else:
+            fan_in = wshape[1]
+        b = 1.0 / math.sqrt(fan_in)
+        sd[name] = rng.uniform(-b, b, shape)
+    return sd
+
+
+def _layer_kind(arch, part, idx):
+    if part == "encoder":
+        return ["conv", "bn", "relu"][idx % 3]
+    if idx == 0:
+        return "linear"
+    if idx == 1:
+        return "bn"
+    if idx < 4:
+        return "other"
+    return ["conv", "bn", "act"][(idx - 4) % 3]
+
+
+def det_inputs(n: int, in_ch: int, hw: int, z_total: int, n_labels: int, seed: int = 1):
+    """x ~ U[0,1) NCHW, labels, eps_c, eps_s ~ N(0,1), CLUB-S permutation (numpy PCG64)."""
+    rng = np.random.default_rng(seed)
+    x = rng.random((n, in_ch, hw, hw))
+    label = rng.integers(0, n_labels, size=n).astype(np.int64)
+    d = z_total // 2
+    eps_c = rng.standard_normal((n, d))
+    eps_s = rng.standard_normal((n, d))
+    perm = rng.permutation(n).astype(np.int64)
+    return x, label, eps_c, eps_s, perm
+
+
+def det_mlp(d: int, hidden_size: int, seed: int = 2) -> dict:
+    """Deterministic estimator weights (mi_estimator.py:111-122 layout, Linear bound 1/sqrt(fan_in))."""
+    rng = np.random.default_rng(seed)
+    h = hidden_size // 2
+    out = {}
+    for net in ("p_mu", "p_logvar"):
+        b1 = 1.0 / math.sqrt(d)
+        out[f"{net}.0.weight"] = rng.uniform(-b1, b1, (h, d))
+        out[f"{net}.0.bias"] = rng.uniform(-b1, b1, (h,))
+        b2 = 1.0 / math.sqrt(h)
+        out[f"{net}.2.weight"] = rng.uniform(-b2, b2, (d, h))
+        out[f"{net}.2.bias"] = rng.uniform(-b2, b2, (d,))
+    return out
+
+
+# ----------------------------------------------------------------------------- functional model
+
+
+def to_torch(sd: dict, dtype=torch.float64, requires_grad=True) -> dict:
+    out = {}
+    for k, v in sd.items():
+        t = torch.as_tensor(np.asarray(v))
+        if k.endswith("num_batches_tracked"):
+            out[k] = t.clone()
+            continue
+        t = t.to(dtype).clone()
+        if requires_grad and not (k.endswith("running_mean") or k.endswith("running_var")):
+            t.requires_grad_(True)
+        out[k] = t
+    return out
+
+
+def _bn(x, P, prefix, train):
+    rm, rv = P[prefix + ".running_mean"], P[prefix + ".running_var"]
+    out = F.batch_norm(x, rm, rv, P[prefix + ".weight"], P[prefix + ".bias"], training=train, momentum=0.1,
+                       eps=1e-5)
+    if train:
+        P[prefix + ".num_batches_tracked"] += 1
+    return out
+
+
+def encode(P, x, arch, train=True):
+    """vae.py:48-50 (encoder 15-26 / 113-130, heads 27-30)."""
+    h = x
+    i = 0
+    for cin, cout, k, s, p in ENC[arch]:
+        h = F.conv2d(h, P[f"encoder.{i}.weight"], P[f"encoder.{i}.bias"], stride=s, padding=p)
+        h = F.relu(_bn(h, P, f"encoder.{i + 1}", train))
+        i += 3
+    h = h.flatten(1)
+    return tuple(F.linear(h, P[f"{n}.weight"], P[f"{n}.bias"]) for n in ("mu_c", "logvar_c", "mu_s", "logvar_s"))
+
+
+def decode(P, z, arch, train=True):
+    """vae.py:52-54 (decoder 32-46 / 136-156)."""
+    h = F.linear(z, P["decoder.0.weight"], P["decoder.0.bias"])
+    h = F.relu(_bn(h, P, "decoder.1", train))
+    h = h.unflatten(1, UNFLAT[arch])
+    i = 4
+    n_dec = len(DEC[arch])
+    for j, (cin, cout, k, s, p, op) in enumerate(DEC[arch]):
+        h = F.conv_transpose2d(h, P[f"decoder.{i}.weight"], P[f"decoder.{i}.bias"], stride=s, padding=p,
+                               output_padding=op)
+        h = _bn(h, P, f"decoder.{i + 1}", train)
+        h = torch.sigmoid(h) if j == n_dec - 1 else F.relu(h)
+        i += 3
+    return h
+
+
+def sample(mu, logvar, eps):
+    """vae.py:56-60 with explicit eps."""
+    return mu + eps * torch.exp(0.5 * logvar)
+
+
+def vae_forward(P, x, eps_c, eps_s, arch, train=True):
+    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, train)
+    z = torch.cat([sample(mu_c, lv_c, eps_c), sample(mu_s, lv_s, eps_s)], dim=-1)
+    return decode(P, z, arch, train), {"mu_c": mu_c, "logvar_c": lv_c, "mu_s": mu_s, "logvar_s": lv_s}, z
+
+
+# ----------------------------------------------------------------------------- losses
+
+
+def vae_loss(xhat, x, mu_c, mu_s, logvar_c, logvar_s):
+    """losses.py:41-50"""
+    def red(t):
+        return t.sum(dim=list(range(t.dim()))[1:]).mean()
+    rec = red((xhat - x) ** 2)
+    kl_c = -0.5 * red(1 + logvar_c - mu_c.pow(2) - logvar_c.exp())
+    kl_s = -0.5 * red(1 + logvar_s - mu_s.pow(2) - logvar_s.exp())
+    return rec, kl_c, kl_s
+
+
+def pairwise(sim_fn, mu, logvar):
+    """losses.py:53-84 and the dispatch at :111-123"""
+    if sim_fn == "cosine":
+        return F.cosine_similarity(mu[None, :, :], mu[:, None, :], dim=-1)
+    if sim_fn == "l2":
+        return -((mu[None, :, :] - mu[:, None, :]) ** 2).sum(dim=-1)
+    if sim_fn == "modified_l2":
+        var = (0.5 * (logvar[None, :, :] + logvar[:, None, :])).exp()
+        return -((mu[None, :, :] - mu[:, None, :]) ** 2 / var).sum(dim=-1)
+    if sim_fn == "jeffrey":
+        k = mu.shape[1]
+        var = logvar.exp()
+        t1 = logvar.sum(dim=-1)[None, :] - logvar.sum(dim=-1)[:, None] - k
+        t2 = ((mu[None, :, :] - mu[:, None, :]) ** 2 / logvar.exp()).sum(dim=-1)
+        t3 = (var[None, :, :] / (var[:, None, :] + 1e-8)).sum(dim=-1)
+        kl = 0.5 * (t1 + t2 + t3)
+        return -(0.5 * (kl + kl.T))
+    if sim_fn == "mahalanobis":
+        var = 0.5 * (logvar.exp()[None, :, :] + logvar.exp()[:, None, :])
+        return -((mu[None, :, :] - mu[:, None, :]) ** 2 / var).sum(dim=-1)
+    raise ValueError("unimplemented similarity measure.")
+
+
+def logsumexp(x, dim):
+    """losses.py:87-95"""
+    m, _ = x.max(dim=dim)
+    mask = m == -float("inf")
+    s = (x - m.masked_fill(mask, 0).unsqueeze(dim)).exp().sum(dim=dim)
+    return s.masked_fill(mask, 1).log() + m.masked_fill(mask, -float("inf"))
+
+
+def snn_loss(sim, pair_mat, temperature):
+    """losses.py:129-137 (out-of-place)"""
+    n = sim.shape[0]
+    eye = torch.eye(n, dtype=torch.bool)
+    sim = sim.masked_fill(eye, float("-inf"))
+    pos = (pair_mat * sim).masked_fill(pair_mat == 0, float("-inf"))
+    return -logsumexp(pos / temperature, dim=1) + logsumexp(sim / temperature, dim=1)
+
+
+def contrastive_loss(mu, logvar, label, sim_fn, temperature, ps=False):
+    """losses.py:98-126"""
+    if ps:
+        pair = (label[None, :] != label[:, None]).to(mu.dtype)
+    else:
+        pair = (label[None, :] == label[:, None]).to(mu.dtype)
+    losses = snn_loss(pairwise(sim_fn, mu, logvar), pair, temperature)
+    return losses[torch.isfinite(losses)].mean()
+
+
+def mlp_forward(M, x):
+    """q(y|x) MLPs (mi_estimator.py:111-127)"""
+    mu = F.linear(F.relu(F.linear(x, M["p_mu.0.weight"], M["p_mu.0.bias"])), M["p_mu.2.weight"], M["p_mu.2.bias"])
+    lv = torch.tanh(F.linear(F.relu(F.linear(x, M["p_logvar.0.weight"], M["p_logvar.0.bias"])),
+                             M["p_logvar.2.weight"], M["p_logvar.2.bias"]))
+    return mu, lv
+
+
+def club_sample(M, x, y, perm):
+    """CLUBSample.forward (mi_estimator.py:133-143) with the permutation passed in."""
+    mu, lv = mlp_forward(M, x)
+    positive = -((mu - y) ** 2) / lv.exp()
+    negative = -((mu - y[perm]) ** 2) / lv.exp()
+    return (positive.sum(dim=-1) - negative.sum(dim=-1)).mean() / 2.0
+
+
+def l1out(M, x, y):
+    """L1OutUB.forward (mi_estimator.py:170-191) including the [N,N,N] broadcast of diag_mask."""
+    n = y.shape[0]
+    mu, lv = mlp_forward(M, x)
+    positive = (-((mu - y) ** 2) / 2.0 / lv.exp() - lv / 2.0).sum(dim=-1)
+    all_probs = (-((y.unsqueeze(0) - mu.unsqueeze(1)) ** 2) / 2.0 / lv.unsqueeze(1).exp()
+                 - lv.unsqueeze(1) / 2.0).sum(dim=-1)
+    diag_mask = torch.ones([n], dtype=x.dtype).diag().unsqueeze(-1) * (-20.0)
+    negative = logsumexp(all_probs + diag_mask, dim=0) - (torch.tensor(n) - 1.0).log().to(x.dtype)
+    return (positive - negative).mean()
+
+
+def learning_loss(M, x, y):
+    """-loglikeli (mi_estimator.py:129-131)"""
+    mu, lv = mlp_forward(M, x)
+    return -((-((mu - y) ** 2) / lv.exp() - lv).sum(dim=1).mean(dim=0))
+
+
+def anneal_weight(step, beta, loc=0, scale=1):
+    """LogisticAnnealer.slope (trainer.py:32-34)"""
+    return beta / (1 + math.exp(-(step - loc) / scale))
+
+
+# ----------------------------------------------------------------------------- one training step
+
+
+def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0):
+    """One CLEARVAETrainer step's losses and gradients (trainer.py:452-482), no optimizer update."""
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True)
+    rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
+    c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
+    s = contrastive_loss(lp["mu_s"], lp["logvar_s"], label, sim_fn, hp["temperature"], ps=hp["ps"])
+    if not hp["ps"]:
+        s = -s
+    w = anneal_weight(step, hp["beta"], hp.get("loc", 0), hp.get("scale", 1))
+    loss = rec + w * kl_c + w * kl_s + hp["alpha"] * c + hp["alpha"] * s
+    params = {k: v for k, v in P.items() if isinstance(v, torch.Tensor) and v.requires_grad}
+    grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
+    return {
+        "xhat": xhat, "z": z, **lp, "rec": rec, "kl_c": kl_c, "kl_s": kl_s, "c_loss": c, "s_loss": s, "loss": loss,
+        "grads": {k: g for k, g in zip(params, grads)},
+    }
+
+
+def mim_step(P, M, x, label, eps_c, eps_s, perm, arch, hp, kind="CLUBSample", sim_fn="cosine", step=0):
+    """The VAE half of one ClearMIMVAETrainer step (trainer.py:848-869): losses and VAE grads."""
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True)
+    rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
+    c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
+    d = z.shape[1] // 2
+    mi = club_sample(M, z[:, :d], z[:, d:], perm) if kind == "CLUBSample" else l1out(M, z[:, :d], z[:, d:])
+    w = anneal_weight(step, hp["beta"], hp.get("loc", 0), hp.get("scale", 1))
+    loss = rec + w * kl_c + w * kl_s + hp["alpha"] * c + hp["lambda"] * mi
+    params = {k: v for k, v in P.items() if isinstance(v, torch.Tensor) and v.requires_grad}
+    grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
+    return {"xhat": xhat, "z": z, **lp, "rec": rec, "kl_c": kl_c, "kl_s": kl_s, "c_loss": c, "mi": mi,
+            "loss": loss, "grads": {k: g for k, g in zip(params, grads)}}
