@@ -146,11 +146,13 @@ class ClearStep:
         self.hp = dict(hp)
         self.sim = SIM[trainer.sim_fn]
         self.anneal = torch.tensor([trainer.annealer.current_step], dtype=torch.int64, device=self.device)
+        self.anneal_expected = trainer.annealer.current_step
         self.seed, _ = rng.offset_tensor(self.device)
         self.offset = torch.zeros(2, dtype=torch.int64, device=self.device)
         self.world = _dist_world()
         self.gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
         self.graphs = {}  # n -> dict
+        self.graphs_enabled = True
         self.steps_since_sync = 0
         if mode == "mim":
             self.est = trainer.mi_estimator
@@ -176,17 +178,34 @@ class ClearStep:
             return False
         if self.mode == "mim" and not self.est_arena.valid():
             return False
-        if self.anneal_host() != self.trainer.annealer.current_step:
+        if self.anneal_expected != self.trainer.annealer.current_step:  # annealer changed by the caller
             self.anneal.fill_(self.trainer.annealer.current_step)
+            self.anneal_expected = self.trainer.annealer.current_step
         return True
-
-    def anneal_host(self):
-        return self.trainer.annealer.current_step  # device counter mirrors the host one (same increments)
 
     def accepts(self, X) -> bool:
         sp = self.spec
         return (X.device.type == "cuda" and X.dim() == 4 and tuple(X.shape[1:]) == (sp.in_ch, sp.H, sp.W)
                 and X.shape[0] >= 2)
+
+    def resync_from_host(self):
+        """After steps taken outside the engine (module path / torch Adam), adopt the host counters."""
+        self.sync_host_state()
+        st = self.trainer.optimizer.state.get(self.arena.params[0], {})
+        if "step" in st:
+            k = int(float(st["step"]))
+            self.adam.host_steps = k
+            self.adam.step.fill_(0)
+            self.adam.step[0] = k
+        for p in self.arena.params:
+            p.grad = self.arena.gview(p)
+        if self.mode == "mim":
+            st = self.trainer.mi_estimator_optimizer.state.get(self.est_arena.params[0], {})
+            if "step" in st:
+                k = int(float(st["step"]))
+                self.est_adam.host_steps = k
+                self.est_adam.step.fill_(0)
+                self.est_adam.step[0] = k
 
     def sync_host_state(self):
         if self.steps_since_sync:
@@ -205,13 +224,21 @@ class ClearStep:
         hp = self.hp
         d = sp.d
         pg = A.gptr
-        fwd = Program()
-        fwd.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-        fwd.add("cv_zero", A.grad, A.numel * 4)
-        ws.encoder_program(fwd, X, True)
-        ws.reparam_program(fwd, None, self.seed, self.offset)
-        ws.decoder_program(fwd, ws.z, True, "loss", X)
-        ws.running_program(fwd, "all")
+        nslot = 6 if self.mode == "mim" else 1
+        eps_buf = torch.zeros(nslot, n, 2 * d, dtype=torch.float32, device=self.device)  # test injection
+        perm_buf = torch.zeros(n, dtype=torch.int64, device=self.device)
+
+        def make_fwd(inject: bool):
+            f = Program()
+            f.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+            f.add("cv_zero", A.grad, A.numel * 4)
+            ws.encoder_program(f, X, True)
+            ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
+            ws.decoder_program(f, ws.z, True, "loss", X)
+            ws.running_program(f, "all")
+            return f
+
+        fwd, fwd_inj = make_fwd(False), make_fwd(True)
         # decoder backward (bucket 1 of the gradient arena)
         dec = Program()
         ws.decoder_backward_program(dec, pg, ws.dz)
@@ -234,52 +261,79 @@ class ClearStep:
                                              ws.lse[1].data_ptr()))
         arr = (cv_ntxent_branch * len(branches))(*branches)
         lat.add("cv_ntxent", arr, len(branches), lab, n, d, self.sim, ctypes.c_float(tau), 2, 1)
+        lat_inj = Program()
+        lat_inj.extend(lat)
         if self.mode == "mim":
             mlp = mlp_struct(self.est)
             zp = ws.z.data_ptr()
-            lat.add("cv_mi_forward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, None, ctypes.c_uint64(self.seed),
-                    self.offset, ws.mi_work, ws.losses.data_ptr() + 20)
-            lat.add("cv_mi_backward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work, None,
-                    ctypes.c_float(float(hp["lambda"])), None, None, 0, 1, None, ws.heads, ws.z, ws.dheads, d)
+            for prog, pin in ((lat, None), (lat_inj, perm_buf)):
+                prog.add("cv_mi_forward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, pin,
+                         ctypes.c_uint64(self.seed), self.offset, ws.mi_work, ws.losses.data_ptr() + 20)
+                prog.add("cv_mi_backward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work, None,
+                         ctypes.c_float(float(hp["lambda"])), None, None, 0, 1, None, ws.heads, ws.z, ws.dheads, d)
         enc = Program()
         ws.encoder_backward_program(enc, pg, ws.dheads, x=X)
         ws.bn_grads_program(enc, pg, "enc")
         upd = Program()
         upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper, self.adam.step,
                 self.gscale if self.world > 1 else None, self.anneal)
-        learn = None
+        learn = learn_inj = None
         if self.mode == "mim":
-            learn = Program()
             E = self.est_arena
             mlp = mlp_struct(self.est)
             G = cv_mlp_grad(*[E.gptr(p) for p in est_params(self.est)])
             zp = ws.z.data_ptr()
-            for j in range(5):
-                learn.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-                ws.encoder_program(learn, X, True)
-                ws.reparam_program(learn, None, self.seed, self.offset)
-                ws.decoder_program(learn, ws.z, True, "none")
-                ws.running_program(learn, "all")
-                learn.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n,
-                          self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
-                          E.numel, self.est_adam.hyper, self.est_adam.step)
-        return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, upd=upd, learn=learn)
+
+            def make_learn(inject: bool):
+                lp = Program()
+                for j in range(5):
+                    lp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+                    ws.encoder_program(lp, X, True)
+                    ws.reparam_program(lp, eps_buf[1 + j] if inject else None, self.seed, self.offset)
+                    ws.decoder_program(lp, ws.z, True, "none")
+                    ws.running_program(lp, "all")
+                    lp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n,
+                           self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
+                           E.numel, self.est_adam.hyper, self.est_adam.step)
+                return lp
+
+            learn, learn_inj = make_learn(False), make_learn(True)
+        return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, upd=upd, learn=learn,
+                    fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf)
 
     def _bucket_split(self):
         """Offset of the first decoder parameter in the arena (decoder grads = [split, numel))."""
         sp = self.spec
         return self.arena.offset[id(sp.dec_lin.weight)][0]
 
-    def _run_eager(self, G):
+    def _run_eager(self, G, inject=False):
         s = _lib.stream_handle()
-        G["fwd"].run(s)
+        G["fwd_inj" if inject else "fwd"].run(s)
         G["dec"].run(s)
-        G["lat"].run(s)
+        G["lat_inj" if inject else "lat"].run(s)
         G["enc"].run(s)
         self._reduce()
         G["upd"].run(s)
         if G["learn"] is not None:
-            G["learn"].run(s)
+            G["learn_inj" if inject else "learn"].run(s)
+
+    def _take_injections(self, G) -> bool:
+        """Consume queued test noise (cvhip.rng): eps_c, eps_s for the main forward and, in CLEAR-MIM,
+        5 more pairs for the estimator forwards; plus one CLUB-S permutation."""
+        need = 2 * (6 if self.mode == "mim" else 1)
+        if rng.pending_noise() < need:
+            return False
+        d = self.spec.d
+        for slot in range(need // 2):
+            ec, es = rng.next_noise(), rng.next_noise()
+            G["eps_buf"][slot, :, :d].copy_(ec)
+            G["eps_buf"][slot, :, d:].copy_(es)
+        if self.mode == "mim":
+            pm = rng.next_perm()
+            if pm is None:
+                raise RuntimeError("CLEAR-MIM injection needs a permutation (cvhip.rng.inject_perm)")
+            G["perm_buf"].copy_(pm)
+        return True
 
     def _reduce(self):
         if self.world > 1:
@@ -323,7 +377,8 @@ class ClearStep:
             self.est_adam.refresh_hyper()
         G["X"].copy_(X, non_blocking=True)
         G["lab"].copy_(label.reshape(-1), non_blocking=True)
-        use_graph = G["count"] >= 1 and not rng.pending_noise()
+        inject = self._take_injections(G)
+        use_graph = G["count"] >= 1 and not inject and self.graphs_enabled
         if use_graph and "graphs" not in G:
             self._capture(G)
         if use_graph:
@@ -334,9 +389,10 @@ class ClearStep:
                 self._reduce()
                 G["graphs"][1].replay()
         else:
-            self._run_eager(G)
+            self._run_eager(G, inject)
         G["count"] += 1
         self.steps_since_sync += 1
+        self.anneal_expected += 1
         ws = G["ws"]
         if self.mode == "mim":
             return ws.losses, self.learn.clone()

@@ -158,12 +158,19 @@ class CLEARVAETrainer(VAETrainer, _ClearEval):
             for batch in bar:
                 X, label = _batch(batch, self.device, self.transform)
                 if engine is not None and engine.accepts(X):
+                    if getattr(self, "_resync", False):
+                        engine.resync_from_host()
+                        self._resync = False
                     losses = engine.step(X, label)
                     self.annealer.step()
                     if verbose:
                         v = losses.tolist()
-                        bar.set_postfix(recontr_loss=v[0], kl_c=v[1], kl_s=v[2], c_loss=v[3], s_loss=v[4])
+                        s_loss = v[4] if hp["ps"] else -v[4]
+                        bar.set_postfix(recontr_loss=v[0], kl_c=v[1], kl_s=v[2], c_loss=v[3], s_loss=s_loss)
                     continue
+                if engine is not None:
+                    engine.sync_host_state()
+                    self._resync = True
                 self.optimizer.zero_grad()
                 X_hat, lp = vae(X)
                 rec, kl_c, kl_s = vae_loss(X_hat, X, **lp)
@@ -181,6 +188,8 @@ class CLEARVAETrainer(VAETrainer, _ClearEval):
                 if verbose:
                     bar.set_postfix(recontr_loss=float(rec), kl_c=float(kl_c), kl_s=float(kl_s),
                                     c_loss=float(c_loss), s_loss=float(s_loss))
+        if engine is not None:
+            engine.sync_host_state()
 
     def evaluate(self, dataloader, verbose, epoch_id):
         hp = self.hyperparameter
@@ -241,13 +250,19 @@ class ClearMIMVAETrainer(VAETrainer, _ClearEval):
             for batch in bar:
                 X, label = _batch(batch, self.device, self.transform)
                 if engine is not None and engine.accepts(X):
+                    if getattr(self, "_resync", False):
+                        engine.resync_from_host()
+                        self._resync = False
                     losses, learn = engine.step(X, label)
                     self.annealer.step()
-                    dev_log.append((losses[5:6], learn))
+                    dev_log.append((losses[5:6].clone(), learn))
                     if verbose:
                         v = losses.tolist()
                         bar.set_postfix(recontr_loss=v[0], kl_c=v[1], kl_s=v[2], c_loss=v[3], mi_loss=v[5])
                     continue
+                if engine is not None:
+                    engine.sync_host_state()
+                    self._resync = True
                 X_hat, lp, z = vae(X, explicit=True)
                 self.optimizer.zero_grad()
                 rec, kl_c, kl_s = vae_loss(X_hat, X, **lp)
@@ -272,6 +287,8 @@ class ClearMIMVAETrainer(VAETrainer, _ClearEval):
                 if verbose:
                     bar.set_postfix(recontr_loss=float(rec), kl_c=float(kl_c), kl_s=float(kl_s),
                                     c_loss=float(c_loss), mi_loss=float(mi))
+        if engine is not None:
+            engine.sync_host_state()
         if dev_log:
             mis = torch.cat([m for m, _ in dev_log]).tolist()
             lls = torch.cat([ll for _, ll in dev_log]).tolist()
