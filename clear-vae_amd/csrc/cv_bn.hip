@@ -244,102 +244,92 @@ static int elem_grid(long total) {
 }
 
 // ---------------------------------------------------------------- decoder Linear -> BN1d backward
-// Block = 64 features (PyTorch order f); phase 1 masks da in place and reduces the BN1d backward
-// sums over the whole batch; phase 2 forms dW[f][k] = sum_n BNbwd(dz)[n][f] * z[n][k].
+// (1) mask + BN1d backward sums: block = 64 features x 64 rows, fp64 atomics into 8 replicas;
+// (2) dW[f][k] += sum_n BNbwd(dz)[n][f] * z[n][k]: block = 64 features x 64 rows staged in LDS.
 constexpr int DL_F = 64;
-constexpr int DL_NCH = 64;   // batch rows per LDS chunk
-constexpr int DL_KMAX = 128; // latent width limit
+constexpr int DL_R = 64;
 
-__global__ __launch_bounds__(256) void declinear_bwd_kernel(int n, int F, int K, int pix, int ch, float* da,
-                                                            const float* __restrict__ h, const cv_bn b, double* gstat,
-                                                            const float* __restrict__ z, float* __restrict__ gw) {
-  __shared__ float sd[DL_NCH][DL_F + 1];
-  __shared__ float sz[DL_NCH][DL_KMAX + 1];
+__global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int pix, int ch, float* da,
+                                                             const float* __restrict__ h, const cv_bn b,
+                                                             double* gstat) {
   __shared__ float r1[4][DL_F], r2[4][DL_F];
   __shared__ BnFwdC kf[DL_F];
-  __shared__ BnBwdC kb[DL_F];
   const int t = threadIdx.x;
-  const int f0 = blockIdx.x * DL_F;
-  if (t < DL_F && f0 + t < F) {
-    kf[t] = bn_fwd_const(b, f0 + t);
-    float m_, i_;
-    bn_mean_istd(b, f0 + t, m_, i_);
-    kb[t].mu = m_;
-    kb[t].istd = i_;
-    kb[t].sc = kf[t].sc;
-  }
+  const int f0 = blockIdx.x * DL_F, rbase = blockIdx.y * DL_R;
+  if (t < DL_F && f0 + t < F) kf[t] = bn_fwd_const(b, f0 + t);
   __syncthreads();
-  // phase 1
-  {
-    const int fl = t % DL_F, rg = t / DL_F;
-    const int f = f0 + fl;
-    float s1 = 0.f, s2 = 0.f;
-    if (f < F) {
-      const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
-      for (int r = rg; r < n; r += 4) {
-        const size_t off = (size_t)r * F + col;
-        const float hv = h[off];
-        float d = da[off];
-        if (bn_out(hv, kf[fl]) <= 0.f) d = 0.f;
-        da[off] = d;
-        s1 += d;
-        s2 += d * ((hv - kb[fl].mu) * kb[fl].istd);
-      }
+  const int fl = t % DL_F, rg = t / DL_F;
+  const int f = f0 + fl;
+  float s1 = 0.f, s2 = 0.f;
+  if (f < F) {
+    const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
+    const BnFwdC k = kf[fl];
+    for (int r = rbase + rg; r < min(n, rbase + DL_R); r += 4) {
+      const size_t off = (size_t)r * F + col;
+      const float hv = h[off];
+      float d = da[off];
+      if (bn_out(hv, k) <= 0.f) d = 0.f;
+      da[off] = d;
+      s1 += d;
+      s2 += d * ((hv - k.mu) * k.istd);
     }
-    r1[rg][fl] = s1;
-    r2[rg][fl] = s2;
   }
+  r1[rg][fl] = s1;
+  r2[rg][fl] = s2;
   __syncthreads();
   if (t < DL_F && f0 + t < F) {
     const double a = (double)r1[0][t] + r1[1][t] + r1[2][t] + r1[3][t];
     const double q = (double)r2[0][t] + r2[1][t] + r2[2][t] + r2[3][t];
-    gstat[f0 + t] = a;
-    gstat[F + f0 + t] = q;
-    kb[t].c1 = (float)(a / (double)b.count);
-    kb[t].c2 = (float)(q / (double)b.count);
+    const int repl = blockIdx.y % CV_STAT_REPL;
+    atomic_add_f64(gstat + (size_t)repl * 2 * F + f0 + t, a);
+    atomic_add_f64(gstat + (size_t)repl * 2 * F + F + f0 + t, q);
+  }
+}
+
+template <int KPT>
+__global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int K, int pix, int ch,
+                                                              const float* __restrict__ dz,
+                                                              const float* __restrict__ h, const cv_bn b,
+                                                              const float* __restrict__ z, float* gw) {
+  __shared__ float sd[DL_R][DL_F + 1];
+  __shared__ float sz[DL_R][4 * KPT + 1];
+  __shared__ BnBwdC kb[DL_F];
+  const int t = threadIdx.x;
+  const int f0 = blockIdx.x * DL_F, r0 = blockIdx.y * DL_R;
+  if (t < DL_F && f0 + t < F) kb[t] = bn_bwd_const(b, f0 + t);
+  __syncthreads();
+  for (int e = t; e < DL_R * DL_F; e += 256) {
+    const int rr = e / DL_F, ff = e % DL_F;
+    const int r = r0 + rr, f = f0 + ff;
+    float v = 0.f;
+    if (r < n && f < F) {
+      const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
+      const size_t off = (size_t)r * F + col;
+      v = bn_bwd(dz[off], h[off], kb[ff]);
+    }
+    sd[rr][ff] = v;
+  }
+  for (int e = t; e < DL_R * K; e += 256) {
+    const int rr = e / K, kk = e % K;
+    const int r = r0 + rr;
+    sz[rr][kk] = (r < n) ? z[(size_t)r * K + kk] : 0.f;
   }
   __syncthreads();
-  // phase 2: each thread owns outputs (f = f0 + t % 64, k = t / 64 + 4j)
   const int fl = t % DL_F, kg = t / DL_F;
-  constexpr int KPT = DL_KMAX / 4;
   float acc[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) acc[j] = 0.f;
-  for (int r0 = 0; r0 < n; r0 += DL_NCH) {
-    __syncthreads();
-    // stage BN-backward dz for 64 rows x 64 features
-    for (int e = t; e < DL_NCH * DL_F; e += 256) {
-      const int rr = e / DL_F, ff = e % DL_F;
-      const int r = r0 + rr, f = f0 + ff;
-      float v = 0.f;
-      if (r < n && f < F) {
-        const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
-        const size_t off = (size_t)r * F + col;
-        v = bn_bwd(da[off], h[off], kb[ff]);
-      }
-      sd[rr][ff] = v;
-    }
-    for (int e = t; e < DL_NCH * K; e += 256) {
-      const int rr = e / K, kk = e % K;
-      const int r = r0 + rr;
-      sz[rr][kk] = (r < n) ? z[(size_t)r * K + kk] : 0.f;
-    }
-    __syncthreads();
-    const int rmax = min(DL_NCH, n - r0);
-    for (int rr = 0; rr < rmax; ++rr) {
-      const float dv = sd[rr][fl];
+  const int rmax = min(DL_R, n - r0);
+  for (int rr = 0; rr < rmax; ++rr) {
+    const float dv = sd[rr][fl];
 #pragma unroll
-      for (int j = 0; j < KPT; ++j) {
-        const int kk = kg + 4 * j;
-        if (kk < K) acc[j] = fmaf(dv, sz[rr][kk], acc[j]);
-      }
-    }
+    for (int j = 0; j < KPT; ++j) acc[j] = fmaf(dv, sz[rr][kg + 4 * j], acc[j]);
   }
   if (f0 + fl < F) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
       const int kk = kg + 4 * j;
-      if (kk < K) gw[(size_t)(f0 + fl) * K + kk] = acc[j];
+      if (kk < K) atomicAdd(gw + (size_t)(f0 + fl) * K + kk, acc[j]);
     }
   }
 }
@@ -449,12 +439,28 @@ extern "C" int cv_declinear_backward_weight(const cv_linear* g, float* da, const
                                             double* gstat_out, const float* zin, float* gweight, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(g && da && h && bn && gstat_out && zin && gweight, "declinear_backward_weight: null args");
-  CV_REQUIRE(g->in_features <= DL_KMAX, "declinear_backward_weight: latent width %d > %d", g->in_features,
-             DL_KMAX);
+  CV_REQUIRE(g->in_features <= 128, "declinear_backward_weight: latent width %d > 128", g->in_features);
   CV_REQUIRE(bn->C == g->out_features && bn->train, "declinear_backward_weight: BN1d must be train-mode, C=out");
   const int pix = g->out_pix > 0 ? g->out_pix : 1;
-  hipLaunchKernelGGL(declinear_bwd_kernel, dim3(cdiv(g->out_features, DL_F)), dim3(256), 0, S(stream), g->n,
-                     g->out_features, g->in_features, pix, g->out_ch, da, h, *bn, gstat_out, zin, gweight);
-  CV_LAUNCH_CHECK("declinear_backward_weight");
+  const int F = g->out_features, K = g->in_features;
+  dim3 grid(cdiv(F, DL_F), cdiv(g->n, DL_R));
+  hipLaunchKernelGGL(declinear_mask_kernel, grid, dim3(256), 0, S(stream), g->n, F, pix, g->out_ch, da, h, *bn,
+                     gstat_out);
+  CV_LAUNCH_CHECK("declinear_mask");
+  cv_bn b2 = *bn;
+  b2.gstat = gstat_out;
+  if (K <= 16)
+    hipLaunchKernelGGL(declinear_wgrad_kernel<4>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
+                       b2, zin, gweight);
+  else if (K <= 32)
+    hipLaunchKernelGGL(declinear_wgrad_kernel<8>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
+                       b2, zin, gweight);
+  else if (K <= 64)
+    hipLaunchKernelGGL(declinear_wgrad_kernel<16>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
+                       b2, zin, gweight);
+  else
+    hipLaunchKernelGGL(declinear_wgrad_kernel<32>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
+                       b2, zin, gweight);
+  CV_LAUNCH_CHECK("declinear_wgrad");
   return 0;
 }

@@ -2,28 +2,31 @@
 //
 // One templated main loop serves every dense contraction of the CLEAR-VAE step:
 //   GATHER  : out[small pixel][cs]  = sum_{tap,cb} T(big[pixel*s-p+tap][cb]) * w(cs,cb,tap)
-//             (Conv2d forward, ConvTranspose2d backward-data, the 4 latent heads as a whole-image conv)
+//             (Conv2d forward, ConvTranspose2d backward-data)
 //   SCATTER : out[big pixel][cb]    = sum_{tap,cs} T(small[(pixel+p-tap)/s][cs]) * w(cs,cb,tap)
-//             (Conv2d backward-data, ConvTranspose2d forward, the heads' backward-data), decomposed
-//             into stride^2 parity classes so every class is a dense GEMM with no masked taps
+//             (Conv2d backward-data, ConvTranspose2d forward), decomposed into stride^2 parity classes
+//             so every class is a dense GEMM with no masked taps
 //   WGRAD   : dw(cs,cb,tap)        += sum_{small pixel} T(small[pixel][cs]) * T(big[gather][cb])
-//             (grad_weight of every conv / convT / head), split-K over pixels, fp32 atomics
-//   DENSE   : out[row][col]         = sum_k T(A[row][perm(k)]) * W(k,col)   (decoder Linear)
+//             (grad_weight of every conv / convT / linear), split-K over pixels, fp32 atomics
+//   DENSE   : out[row][col]         = sum_k T(A[row][perm(k)]) * W(k,col)   (Linear layers)
 // T() is the fused BatchNorm(+ReLU) forward or backward transform (cv_common.hpp); BN batch
 // statistics of the produced tensor are reduced in the epilogue (fp64 atomics, 8 replicas).
 //
 // Reference arithmetic replaced: nn.Conv2d / nn.ConvTranspose2d / nn.Linear / nn.BatchNorm2d / ReLU
 // of code/src/models/vae.py:15-46 (VAE) and :113-156 (VAE64), forward and autograd backward.
 //
-// Tile: BM x BN x 16, 256 threads = 4 waves laid out WM x WN; each wave owns (BM/WM) x (BN/WN)
-// as 16x16 MFMA tiles. Operands are staged global -> registers -> LDS (k-major, padded so the
-// ds_read_b32 operand fetches are bank-conflict free), the next tile's global loads are issued
-// before the current tile's MFMAs (register double buffering).
+// Tile: BM x BN x 32, 256 threads = 4 waves laid out WM x WN; each wave owns (BM/WM) x (BN/WN)
+// as 16x16 MFMA tiles.  Operands go global -> registers -> LDS (k-major, padded so the ds_read_b32
+// fragment reads are bank-conflict free); LDS is double-buffered, so a K tile costs one barrier,
+// and the next tile's global loads are in flight during the current tile's MFMAs.  Conv weights
+// are pre-packed once per step (cv_pack_conv_weights) into GEMM-native [K][N] rows, so the B
+// operand is a coalesced float4 stream with no index arithmetic; activation gathers are float4
+// along channels with all integer division hoisted to once per row (rows) or once per K tile.
 #include "cv_common.hpp"
 
 namespace cv {
 
-constexpr int BK = 16;
+constexpr int BK = 32;
 constexpr int NT = 256;
 
 enum { OP_GATHER = 0, OP_SCATTER = 1, OP_WGRAD = 2, OP_DENSE = 3 };
@@ -33,13 +36,12 @@ struct Geo {
   int n, hs, ws, cs, hb, wb, cb, kh, kw, s, p;
 };
 
-// Per-problem arguments (passed by value as the kernel argument).
 struct Args {
   int op;
   Geo g;
   cv_operand a;        // GATHER: big-grid input; SCATTER: small-grid input; WGRAD: small-grid; DENSE: A
   cv_operand b;        // WGRAD: big-grid operand
-  const float* w;      // weights (GATHER/SCATTER/DENSE)
+  const float* w;      // GATHER: packed [tap][cb][cs]; SCATTER: packed [tap][cs][cb]; DENSE: Linear weight
   int wlayout;         // DENSE: 0 -> W[col*ldb + k], 1 -> W[k*ldb + col]
   int ldb;
   const float* bias;
@@ -47,19 +49,15 @@ struct Args {
   float* out;
   int accumulate;      // atomicAdd into out (split-K)
   cv_epilogue ep;
-  int M, N, K;         // GEMM sizes (SCATTER: per class sizes computed in-kernel)
-  int ksplit;          // number of K splits (grid.z for GATHER/WGRAD/DENSE)
+  int M, N, K;         // GEMM sizes (SCATTER: per class sizes computed in-kernel; N excludes bias col)
   int kchunk;          // K elements per split (multiple of BK)
-  // DENSE
-  int lda, a_pix, a_ch;      // A row stride; NCHW-flatten permutation of A columns (a_pix=1: none)
-  int ldo, o_pix, o_ch;      // out row stride; permutation of output columns
-  // constants sizes (LDS)
+  int lda, a_pix, a_ch;      // DENSE: A row stride; NCHW-flatten permutation of A columns (a_pix=1: none)
+  int ldo, o_pix, o_ch;      // DENSE: out row stride; permutation of output columns
   int ca_n, cb_n, ce_n;      // feature counts of a / b / epilogue BN constants (0 = unused)
 };
 
 // ------------------------------------------------------------------ operand transform helpers
 struct XfA {
-  // LDS views of constants
   const BnFwdC* f;
   const BnBwdC* bw;
 };
@@ -68,6 +66,17 @@ __device__ __forceinline__ float xf_apply(const cv_operand& o, const XfA& c, int
   if (o.xf == CV_XF_BNRELU) return bn_relu(x, c.f[ch]);
   if (o.xf == CV_XF_BNBWD) return bn_bwd(x, y, c.bw[ch]);
   return x;
+}
+
+__device__ __forceinline__ float4 xf_apply4(const cv_operand& o, const XfA& c, int ch0, float4 v, const float* yp) {
+  if (o.xf == CV_XF_NONE) return v;
+  float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (o.xf == CV_XF_BNBWD) yy = *reinterpret_cast<const float4*>(yp);
+  v.x = xf_apply(o, c, ch0 + 0, v.x, yy.x);
+  v.y = xf_apply(o, c, ch0 + 1, v.y, yy.y);
+  v.z = xf_apply(o, c, ch0 + 2, v.z, yy.z);
+  v.w = xf_apply(o, c, ch0 + 3, v.w, yy.w);
+  return v;
 }
 
 __device__ __forceinline__ void fill_consts(const cv_operand& o, int nfeat, float* lds, XfA& c) {
@@ -89,6 +98,7 @@ __host__ __device__ inline int xf_floats(int xf, int nfeat) {
 }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 z4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // ------------------------------------------------------------------ the kernel
 template <int BM, int BN>
@@ -98,89 +108,86 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(FM >= 1 && FN >= 1, "tile too small");
-  constexpr int LDA = BM + 16;
+  constexpr int LDA = BM + 16;                              // (BM+16) % 32 == 16: conflict-free reads
   constexpr int LDB = BN + ((BN % 32) == 0 ? 16 : 0);
-  constexpr int AR = BM * BK / NT;  // A floats per thread
-  constexpr int BR = BN * BK / NT;  // B floats per thread (may be < 1 -> handled as 1 with guard)
-  constexpr int BRR = BR > 0 ? BR : 1;
+  constexpr int RA = BM / 32;                               // A rows per thread (row-oriented)
+  constexpr int AW = (BM * BK / 4 + NT - 1) / NT;           // WGRAD A float4 per thread
+  constexpr int BW = (BN * BK / 4 + NT - 1) / NT;           // B float4 per thread
+  constexpr int RAW = RA > AW ? RA : AW;
+  constexpr int ABUF = BK * LDA, BBUF = BK * LDB;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;
-  float* Bs = As + BK * LDA;
-  float* red = Bs + BK * LDB;          // epilogue reduction scratch: 2 * WM * BN floats
-  float* cst = red + 2 * WM * BN;      // BN constants
-  float* cstA = cst;
+  float* As = smem;                     // [2][BK][LDA]
+  float* Bs = As + 2 * ABUF;            // [2][BK][LDB]
+  float* red = Bs + 2 * BBUF;           // epilogue reduction scratch: 2 * WM * BN floats
+  float* cstA = red + 2 * WM * BN;      // BN constants
   float* cstB = cstA + xf_floats(P.a.xf, P.ca_n);
   float* cstE = cstB + xf_floats(P.b.xf, P.cb_n);
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid / WN, wn = wid % WN;
+  const int op = P.op;
 
   // ---------------- block -> (m0, n0, k-range, class)
-  int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  int M = P.M, N = P.N, K = P.K;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int M = P.M, K = P.K;
+  const int N = P.N + ((op == OP_WGRAD && P.gbias) ? 1 : 0);
   int kbeg = 0, kend = K;
-  // SCATTER class data
-  int ry = 0, rx = 0, yb0 = 0, xb0 = 0, cy = 1, cx = 1, nty = 1, ntx = 1;
-  if (P.op == OP_SCATTER) {
-    const int s = P.g.s;
-    const int cls = blockIdx.z;
+  int ry = 0, rx = 0, yb0 = 0, xb0 = 0, cy = 1, cx = 1, ntx = 1;
+  if (op == OP_SCATTER) {
+    const int s = P.g.s, cls = blockIdx.z;
     ry = cls / s;
     rx = cls % s;
-    // big rows with (yb + p) % s == ry
-    yb0 = (((ry - P.g.p) % s) + s) % s;
+    yb0 = (((ry - P.g.p) % s) + s) % s;  // big rows with (yb + p) % s == ry
     xb0 = (((rx - P.g.p) % s) + s) % s;
     cy = (P.g.hb > yb0) ? (P.g.hb - yb0 + s - 1) / s : 0;
     cx = (P.g.wb > xb0) ? (P.g.wb - xb0 + s - 1) / s : 0;
-    nty = (P.g.kh > ry) ? (P.g.kh - ry + s - 1) / s : 0;
+    const int nty = (P.g.kh > ry) ? (P.g.kh - ry + s - 1) / s : 0;
     ntx = (P.g.kw > rx) ? (P.g.kw - rx + s - 1) / s : 0;
     M = P.g.n * cy * cx;
     K = nty * ntx * P.g.cs;
     kend = K;
     if (m0 >= M) return;
   } else {
-    const int z = blockIdx.z;
-    kbeg = z * P.kchunk;
+    kbeg = blockIdx.z * P.kchunk;
     kend = min(K, kbeg + P.kchunk);
     if (kbeg >= kend) return;
   }
 
   // ---------------- prologue: BN constants into LDS
-  XfA ca, cb, ce;
+  XfA ca, cb;
   fill_consts(P.a, P.ca_n, cstA, ca);
   fill_consts(P.b, P.cb_n, cstB, cb);
-  ce.f = nullptr;
-  ce.bw = nullptr;
   if (P.ep.stat_mode == CV_STAT_BWD) {
     BnFwdC* d = reinterpret_cast<BnFwdC*>(cstE);
     for (int i = t; i < P.ce_n; i += NT) d[i] = bn_fwd_const(P.ep.ebn, i);
   }
-  __syncthreads();
 
-  // ---------------- per-thread A-row decode (row-oriented problems)
-  constexpr int RA = (BM >= 64) ? BM / 64 : 1;
+  // ---------------- per-thread A-row decode (row-oriented problems): rows (t&15)+16*(t>>7)+32*i,
+  // K quad (t>>4)&7 of the 32-deep tile
+  const int quad = (t >> 4) & 7;
   int r_n[RA], r_y[RA], r_x[RA];
   bool r_ok[RA];
-  const int quad = (t >> 4) & 3;
-  if (P.op == OP_GATHER || P.op == OP_SCATTER || P.op == OP_DENSE) {
+  if (op != OP_WGRAD) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
-      const int r = m0 + (t & 15) + 16 * (t >> 6) + 64 * i;
-      r_ok[i] = (r < M) && (BM >= 64 || (t >> 6) < BM / 16);
+      const int r = m0 + (t & 15) + 16 * (t >> 7) + 32 * i;
+      r_ok[i] = r < M;
       const int rr = r_ok[i] ? r : 0;
-      if (P.op == OP_GATHER) {
+      if (op == OP_GATHER) {
         const int hw = P.g.hs * P.g.ws;
         r_n[i] = rr / hw;
         const int rem = rr - r_n[i] * hw;
-        r_y[i] = rem / P.g.ws;
-        r_x[i] = rem - r_y[i] * P.g.ws;
-      } else if (P.op == OP_SCATTER) {
+        const int ys = rem / P.g.ws, xs = rem - ys * P.g.ws;
+        r_y[i] = ys * P.g.s - P.g.p;  // big-grid origin of the receptive field
+        r_x[i] = xs * P.g.s - P.g.p;
+      } else if (op == OP_SCATTER) {
         const int hw = cy * cx;
         r_n[i] = rr / hw;
         const int rem = rr - r_n[i] * hw;
         const int ty = rem / cx, tx = rem - ty * cx;
-        r_y[i] = yb0 + P.g.s * ty;  // big-grid coordinates
-        r_x[i] = xb0 + P.g.s * tx;
+        r_y[i] = yb0 + P.g.s * ty + P.g.p;  // (yb + p); ys = (r_y - kh) / s
+        r_x[i] = xb0 + P.g.s * tx + P.g.p;
       } else {
         r_n[i] = rr;
         r_y[i] = 0;
@@ -188,142 +195,131 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
       }
     }
   }
+  __syncthreads();
 
-  float ra[AR], rb[BRR];
+  float4 ra[RAW];
+  float4 rb[BW];
 
   // ---------------- operand fetchers
   auto fetchA = [&](int k0) {
-    if (P.op == OP_GATHER) {
-      const Geo& g = P.g;
+    const Geo& g = P.g;
+    if (op == OP_GATHER) {
       const int kq = k0 + 4 * quad;
-      const bool vec = (g.cb % 4) == 0 && !P.a.nchw;
+      if ((g.cb & 3) == 0 && !P.a.nchw) {
+        // the 4 k of this quad share one tap: one division per tile
+        const int tap = kq / g.cb, c0 = kq - tap * g.cb;
+        const int kh = tap / g.kw, kw = tap - kh * g.kw;
 #pragma unroll
-      for (int i = 0; i < RA; ++i) {
-        if (vec) {
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r_ok[i] && kq < kend) {
-            const int tap = kq / g.cb, c0 = kq - tap * g.cb;
-            const int kh = tap / g.kw, kw = tap - kh * g.kw;
-            const int yb = r_y[i] * g.s - g.p + kh, xb = r_x[i] * g.s - g.p + kw;
-            if (yb >= 0 && yb < g.hb && xb >= 0 && xb < g.wb) {
-              const size_t off = ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
-              v = ld4(P.a.x + off);
-              if (P.a.xf != CV_XF_NONE) {
-                float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (P.a.xf == CV_XF_BNBWD) yy = ld4(P.a.y + off);
-                v.x = xf_apply(P.a, ca, c0 + 0, v.x, yy.x);
-                v.y = xf_apply(P.a, ca, c0 + 1, v.y, yy.y);
-                v.z = xf_apply(P.a, ca, c0 + 2, v.z, yy.z);
-                v.w = xf_apply(P.a, ca, c0 + 3, v.w, yy.w);
-              }
-            }
+        for (int i = 0; i < RA; ++i) {
+          float4 v = z4();
+          const int yb = r_y[i] + kh, xb = r_x[i] + kw;
+          if (r_ok[i] && kq < kend && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
+            const size_t off = ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
+            v = xf_apply4(P.a, ca, c0, ld4(P.a.x + off), P.a.y + off);
           }
-          ra[4 * i + 0] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
-        } else {
+          ra[i] = v;
+        }
+      } else {  // first conv (C = 1 or 3, NCHW input) / last convT backward (C = 1 or 3)
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          float tmp[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float v = 0.f;
+            tmp[j] = 0.f;
             const int k = kq + j;
             if (r_ok[i] && k < kend) {
               const int tap = k / g.cb, c = k - tap * g.cb;
               const int kh = tap / g.kw, kw = tap - kh * g.kw;
-              const int yb = r_y[i] * g.s - g.p + kh, xb = r_x[i] * g.s - g.p + kw;
-              if (yb >= 0 && yb < g.hb && xb >= 0 && xb < g.wb) {
+              const int yb = r_y[i] + kh, xb = r_x[i] + kw;
+              if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
                 const size_t off = P.a.nchw ? ((size_t)(r_n[i] * g.cb + c) * g.hb + yb) * g.wb + xb
                                             : ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c;
                 const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
-                v = xf_apply(P.a, ca, c, P.a.x[off], yv);
+                tmp[j] = xf_apply(P.a, ca, c, P.a.x[off], yv);
               }
             }
-            ra[4 * i + j] = v;
           }
+          ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         }
       }
-    } else if (P.op == OP_SCATTER) {
-      const Geo& g = P.g;
+    } else if (op == OP_SCATTER) {
       const int kq = k0 + 4 * quad;
-      const bool vec = (g.cs % 4) == 0;
+      if ((g.cs & 3) == 0) {
+        const int tap = kq / g.cs, c0 = kq - tap * g.cs;
+        const int jy = tap / ntx, jx = tap - jy * ntx;
+        const int kh = ry + g.s * jy, kw = rx + g.s * jx;
 #pragma unroll
-      for (int i = 0; i < RA; ++i) {
+        for (int i = 0; i < RA; ++i) {
+          float4 v = z4();
+          const int py = r_y[i] - kh, px = r_x[i] - kw;  // divisible by s by construction
+          if (r_ok[i] && kq < kend && py >= 0 && px >= 0) {
+            const int ys = py / g.s, xs = px / g.s;
+            if (ys < g.hs && xs < g.ws) {
+              const size_t off = ((size_t)(r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c0;
+              v = xf_apply4(P.a, ca, c0, ld4(P.a.x + off), P.a.y + off);
+            }
+          }
+          ra[i] = v;
+        }
+      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (!vec || j == 0) {
+        for (int i = 0; i < RA; ++i) {
+          float tmp[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            tmp[j] = 0.f;
             const int k = kq + j;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (r_ok[i] && k < kend) {
               const int tap = k / g.cs, c = k - tap * g.cs;
               const int jy = tap / ntx, jx = tap - jy * ntx;
-              const int kh = ry + g.s * jy, kw = rx + g.s * jx;
-              const int ys = (r_y[i] + g.p - kh) / g.s, xs = (r_x[i] + g.p - kw) / g.s;
-              if (ys >= 0 && ys < g.hs && xs >= 0 && xs < g.ws &&
-                  (r_y[i] + g.p - kh) >= 0 && (r_x[i] + g.p - kw) >= 0) {
-                const size_t off = ((size_t)(r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c;
-                if (vec) {
-                  v = ld4(P.a.x + off);
-                  if (P.a.xf != CV_XF_NONE) {
-                    float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (P.a.xf == CV_XF_BNBWD) yy = ld4(P.a.y + off);
-                    v.x = xf_apply(P.a, ca, c + 0, v.x, yy.x);
-                    v.y = xf_apply(P.a, ca, c + 1, v.y, yy.y);
-                    v.z = xf_apply(P.a, ca, c + 2, v.z, yy.z);
-                    v.w = xf_apply(P.a, ca, c + 3, v.w, yy.w);
-                  }
-                } else {
-                  const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
-                  v.x = xf_apply(P.a, ca, c, P.a.x[off], yv);
-                }
+              const int py = r_y[i] - (ry + g.s * jy), px = r_x[i] - (rx + g.s * jx);
+              if (py >= 0 && px >= 0 && py / g.s < g.hs && px / g.s < g.ws) {
+                const size_t off = ((size_t)(r_n[i] * g.hs + py / g.s) * g.ws + px / g.s) * g.cs + c;
+                const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
+                tmp[j] = xf_apply(P.a, ca, c, P.a.x[off], yv);
               }
             }
-            if (vec) {
-              ra[4 * i + 0] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
-            } else {
-              ra[4 * i + j] = v.x;
-            }
           }
+          ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         }
       }
-    } else if (P.op == OP_DENSE) {
+    } else if (op == OP_DENSE) {
       const int kq = k0 + 4 * quad;
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
+        float tmp[4];
+        if (P.a_pix == 1 && (P.lda & 3) == 0 && kq + 3 < kend && r_ok[i]) {
+          const size_t off = (size_t)r_n[i] * P.lda + kq;
+          const float4 v = xf_apply4(P.a, ca, kq, ld4(P.a.x + off), P.a.y + off);
+          tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = kq + j;
-          float v = 0.f;
-          if (r_ok[i] && k < kend) {
-            const int col = (P.a_pix > 1) ? (k % P.a_pix) * P.a_ch + k / P.a_pix : k;
-            const size_t off = (size_t)r_n[i] * P.lda + col;
-            const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
-            // constants are per logical feature k (BN1d) or per channel k / a_pix (BN2d)
-            v = xf_apply(P.a, ca, (P.ca_n == K) ? k : k / P.a_pix, P.a.x[off], yv);
+          for (int j = 0; j < 4; ++j) {
+            const int k = kq + j;
+            tmp[j] = 0.f;
+            if (r_ok[i] && k < kend) {
+              const int col = (P.a_pix > 1) ? (k % P.a_pix) * P.a_ch + k / P.a_pix : k;
+              const size_t off = (size_t)r_n[i] * P.lda + col;
+              const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
+              // constants are per logical feature k (BN1d) or per channel k / a_pix (BN2d)
+              tmp[j] = xf_apply(P.a, ca, (P.ca_n == K) ? k : k / P.a_pix, P.a.x[off], yv);
+            }
           }
-          ra[4 * i + j] = v;
         }
+        ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
       }
-    } else {  // OP_WGRAD: A(m = cs, k = small pixel) = T(small[pix][cs]); As[k][m]
-      const Geo& g = P.g;
-      constexpr int MQ = BM / 4;                 // float4 per pixel row of the tile
-      constexpr int PER = (MQ * BK) / NT;        // float4 per thread (>=1 when BM>=64)
-      constexpr int PERR = PER > 0 ? PER : 1;
+    } else {  // OP_WGRAD: A(m = cs, k = small pixel) = T(small[pix][cs]); float4 along cs
+      constexpr int MQ = BM / 4;
 #pragma unroll
-      for (int e = 0; e < PERR; ++e) {
+      for (int e = 0; e < AW; ++e) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
-        const int pix = k0 + kk;
-        const int c0 = m0 + 4 * mq;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int pix = k0 + kk, c0 = m0 + 4 * mq;
+        float4 v = z4();
         if (kk < BK && pix < kend) {
           const size_t off = (size_t)pix * g.cs + c0;
-          if ((g.cs % 4) == 0 && c0 + 3 < g.cs) {
-            v = ld4(P.a.x + off);
-            float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (P.a.xf == CV_XF_BNBWD) yy = ld4(P.a.y + off);
-            if (P.a.xf != CV_XF_NONE) {
-              v.x = xf_apply(P.a, ca, c0 + 0, v.x, yy.x);
-              v.y = xf_apply(P.a, ca, c0 + 1, v.y, yy.y);
-              v.z = xf_apply(P.a, ca, c0 + 2, v.z, yy.z);
-              v.w = xf_apply(P.a, ca, c0 + 3, v.w, yy.w);
-            }
+          if ((g.cs & 3) == 0) {
+            if (c0 < g.cs) v = xf_apply4(P.a, ca, c0, ld4(P.a.x + off), P.a.y + off);
           } else {
             float tmp[4];
 #pragma unroll
@@ -337,73 +333,111 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
             v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
         }
-        ra[4 * e + 0] = v.x; ra[4 * e + 1] = v.y; ra[4 * e + 2] = v.z; ra[4 * e + 3] = v.w;
+        ra[e] = v;
       }
     }
   };
 
-  auto storeA = [&]() {
-    if (P.op == OP_WGRAD) {
+  auto storeA = [&](float* Ab) {
+    if (op == OP_WGRAD) {
       constexpr int MQ = BM / 4;
-      constexpr int PER = (MQ * BK) / NT;
-      constexpr int PERR = PER > 0 ? PER : 1;
 #pragma unroll
-      for (int e = 0; e < PERR; ++e) {
+      for (int e = 0; e < AW; ++e) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
-        if (kk < BK) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) As[kk * LDA + 4 * mq + j] = ra[4 * e + j];
-        }
+        if (kk < BK) *reinterpret_cast<float4*>(Ab + kk * LDA + 4 * mq) = ra[e];
       }
     } else {
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
-        const int m = (t & 15) + 16 * (t >> 6) + 64 * i;
-        if (m < BM) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) As[(4 * quad + j) * LDA + m] = ra[4 * i + j];
-        }
+        const int m = (t & 15) + 16 * (t >> 7) + 32 * i;
+        float* p = Ab + (4 * quad) * LDA + m;
+        p[0] = ra[i].x;
+        p[LDA] = ra[i].y;
+        p[2 * LDA] = ra[i].z;
+        p[3 * LDA] = ra[i].w;
       }
     }
   };
 
+  // B: one float4 of a K row (4 consecutive columns) per slot; rows kk, column quad nq
+  constexpr int NQ = BN / 4;
   auto fetchB = [&](int k0) {
+    const Geo& g = P.g;
 #pragma unroll
-    for (int e = 0; e < BRR; ++e) {
+    for (int e = 0; e < BW; ++e) {
       const int idx = t + NT * e;
-      const int nn = idx % BN, kk = idx / BN;
-      const int col = n0 + nn, k = k0 + kk;
-      float v = 0.f;
-      if (kk < BK && col < N && k < kend) {
-        if (P.op == OP_GATHER) {
-          const Geo& g = P.g;
-          const int tap = k / g.cb, c = k - tap * g.cb;
-          // w(cs=col, cb=c, tap)
-          v = P.w[((size_t)col * g.cb + c) * (g.kh * g.kw) + tap];
-        } else if (P.op == OP_SCATTER) {
-          const Geo& g = P.g;
+      const int nq = idx % NQ, kk = idx / NQ;
+      const int col = n0 + 4 * nq, k = k0 + kk;
+      float4 v = z4();
+      if (kk < BK && k < kend && col < N) {
+        if (op == OP_GATHER) {  // packed [K = tap*cb][cs]
+          if (col + 3 < N && (g.cs & 3) == 0) {
+            v = ld4(P.w + (size_t)k * g.cs + col);
+          } else {
+            float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)k * g.cs + col + j];
+            v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+          }
+        } else if (op == OP_SCATTER) {  // packed [tap][cs][cb]; class taps
           const int tap = k / g.cs, c = k - tap * g.cs;
           const int jy = tap / ntx, jx = tap - jy * ntx;
           const int kh = ry + g.s * jy, kw = rx + g.s * jx;
-          v = P.w[(((size_t)c * g.cb + col) * g.kh + kh) * g.kw + kw];
-        } else if (P.op == OP_DENSE) {
-          v = P.wlayout ? P.w[(size_t)k * P.ldb + col] : P.w[(size_t)col * P.ldb + k];
-        } else if (P.gbias && col == N - 1) {  // WGRAD bias column
-          v = 1.0f;
+          const size_t rowo = ((size_t)(kh * g.kw + kw) * g.cs + c) * g.cb;
+          if (col + 3 < N && (g.cb & 3) == 0) {
+            v = ld4(P.w + rowo + col);
+          } else {
+            float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[rowo + col + j];
+            v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+          }
+        } else if (op == OP_DENSE) {
+          float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+          if (P.wlayout) {
+            if (col + 3 < N && (P.ldb & 3) == 0) {
+              v = ld4(P.w + (size_t)k * P.ldb + col);
+              tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
+            } else {
+              for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)k * P.ldb + col + j];
+            }
+          } else {
+            for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)(col + j) * P.ldb + k];
+          }
+          v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         } else {  // WGRAD: B(k = small pixel, col = (tap, cb)) = T(big[gather(pix, tap)][cb])
-          const Geo& g = P.g;
-          const int tap = col / g.cb, c = col - tap * g.cb;
-          const int kh = tap / g.kw, kw = tap - kh * g.kw;
           const int hw = g.hs * g.ws;
           const int nimg = k / hw, rem = k - nimg * hw;
           const int ys = rem / g.ws, xs = rem - ys * g.ws;
-          const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
-          if (yb >= 0 && yb < g.hb && xb >= 0 && xb < g.wb) {
-            const size_t off = P.b.nchw ? ((size_t)(nimg * g.cb + c) * g.hb + yb) * g.wb + xb
-                                        : ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + c;
-            const float yv = (P.b.xf == CV_XF_BNBWD) ? P.b.y[off] : 0.f;
-            v = xf_apply(P.b, cb, c, P.b.x[off], yv);
+          const int nreal = P.N;
+          if (col >= nreal) {  // bias column (nreal % 4 == 0 when gbias is used)
+            v = make_float4(col == nreal ? 1.f : 0.f, 0.f, 0.f, 0.f);
+          } else if ((g.cb & 3) == 0 && !P.b.nchw) {
+            const int tap = col / g.cb, c0 = col - tap * g.cb;
+            const int kh = tap / g.kw, kw = tap - kh * g.kw;
+            const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
+            if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
+              const size_t off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + c0;
+              v = xf_apply4(P.b, cb, c0, ld4(P.b.x + off), P.b.y + off);
+            }
+          } else {
+            float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 4 && col + j < nreal; ++j) {
+              const int cc = col + j;
+              const int tap = cc / g.cb, c = cc - tap * g.cb;
+              const int kh = tap / g.kw, kw = tap - kh * g.kw;
+              const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
+              if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
+                const size_t off = P.b.nchw ? ((size_t)(nimg * g.cb + c) * g.hb + yb) * g.wb + xb
+                                            : ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + c;
+                const float yv = (P.b.xf == CV_XF_BNBWD) ? P.b.y[off] : 0.f;
+                tmp[j] = xf_apply(P.b, cb, c, P.b.x[off], yv);
+              }
+            }
+            if (P.gbias && col + 3 >= nreal) {
+              for (int j = 0; j < 4; ++j)
+                if (col + j == nreal) tmp[j] = 1.f;
+            }
+            v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
         }
       }
@@ -411,16 +445,16 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     }
   };
 
-  auto storeB = [&]() {
+  auto storeB = [&](float* Bb) {
 #pragma unroll
-    for (int e = 0; e < BRR; ++e) {
+    for (int e = 0; e < BW; ++e) {
       const int idx = t + NT * e;
-      const int nn = idx % BN, kk = idx / BN;
-      if (kk < BK) Bs[kk * LDB + nn] = rb[e];
+      const int nq = idx % NQ, kk = idx / NQ;
+      if (kk < BK) *reinterpret_cast<float4*>(Bb + kk * LDB + 4 * nq) = rb[e];
     }
   };
 
-  // ---------------- main loop
+  // ---------------- main loop (double-buffered LDS, one barrier per K tile)
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -429,29 +463,38 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
 
   fetchA(kbeg);
   fetchB(kbeg);
+  storeA(As);
+  storeB(Bs);
+  __syncthreads();
+  int cur = 0;
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    storeA();
-    storeB();
-    __syncthreads();
-    if (k0 + BK < kend) {
+    const bool more = k0 + BK < kend;
+    if (more) {
       fetchA(k0 + BK);
       fetchB(k0 + BK);
     }
+    const float* Ab = As + cur * ABUF;
+    const float* Bb = Bs + cur * BBUF;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       const int kr = kk + (lane >> 4);
       float av[FM], bv[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) av[i] = As[kr * LDA + wm * TM + i * 16 + (lane & 15)];
+      for (int i = 0; i < FM; ++i) av[i] = Ab[kr * LDA + wm * TM + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bv[j] = Bs[kr * LDB + wn * TN + j * 16 + (lane & 15)];
+      for (int j = 0; j < FN; ++j) bv[j] = Bb[kr * LDB + wn * TN + j * 16 + (lane & 15)];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
+    if (more) {
+      storeA(As + (cur ^ 1) * ABUF);
+      storeB(Bs + (cur ^ 1) * BBUF);
+    }
+    __syncthreads();
+    cur ^= 1;
   }
 
   // ---------------- epilogue
@@ -471,21 +514,20 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
         const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
         float v = acc[i][j][r];
         if (row >= M || col >= N) continue;
-        if (P.op == OP_WGRAD) {
-          if (P.gbias && col == N - 1) {
+        if (op == OP_WGRAD) {
+          if (col >= P.N) {  // bias column
             atomicAdd(P.gbias + row, v);
             continue;
           }
-          // row = cs, col = (tap, cb) -> w layout [cs][cb][kh][kw]
           const Geo& g = P.g;
-          const int tap = col / g.cb, c = col - tap * g.cb;
+          const int tap = col / g.cb, c = col - tap * g.cb;  // w layout [cs][cb][kh][kw]
           atomicAdd(P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap, v);
           continue;
         }
         size_t off;
-        if (P.op == OP_GATHER) {
+        if (op == OP_GATHER) {
           off = (size_t)row * P.g.cs + col;
-        } else if (P.op == OP_SCATTER) {
+        } else if (op == OP_SCATTER) {
           const int hw = cy * cx;
           const int nimg = row / hw, rem = row - nimg * hw;
           const int ty = rem / cx, tx = rem - ty * cx;
@@ -519,7 +561,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     }
   }
 
-  if (stats && !P.accumulate && P.op != OP_WGRAD) {
+  if (stats && !P.accumulate && op != OP_WGRAD) {
     // reduce per column: lanes with equal (lane & 15), then the WM waves sharing wn
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -528,12 +570,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
       s2[j] += __shfl_xor(s2[j], 16, 64);
       s2[j] += __shfl_xor(s2[j], 32, 64);
     }
-    __syncthreads();  // red may alias nothing, but As/Bs are free now
     if (lane < 16) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = wn * TN + j * 16 + lane;
-        red[(wm)*BN + c] = s1[j];
+        red[wm * BN + c] = s1[j];
         red[WM * BN + wm * BN + c] = s2[j];
       }
     }
@@ -557,11 +598,37 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   }
 }
 
+// ------------------------------------------------------------------ weight packing
+// Wg[tap][cb][cs] (GATHER) and Ws[tap][cs][cb] (SCATTER) from w(cs, cb, tap) = W[cs][cb][kh][kw]
+constexpr int MAX_PACK = 16;
+struct PackArgs {
+  const float* src[MAX_PACK];
+  float* dg[MAX_PACK];
+  float* ds[MAX_PACK];
+  int cs[MAX_PACK], cb[MAX_PACK], kk[MAX_PACK];
+  int n;
+};
+__global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
+  const int l = blockIdx.y;
+  if (l >= a.n) return;
+  const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
+  const long total = (long)cs * cbn * kk;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    // i enumerates the source W[cs][cb][tap]
+    const int tap = (int)(i % kk);
+    const long r = i / kk;
+    const int c_b = (int)(r % cbn), c_s = (int)(r / cbn);
+    const float v = a.src[l][i];
+    if (a.dg[l]) a.dg[l][((size_t)tap * cbn + c_b) * cs + c_s] = v;
+    if (a.ds[l]) a.ds[l][((size_t)tap * cs + c_s) * cbn + c_b] = v;
+  }
+}
+
 // ------------------------------------------------------------------ host-side launch
 static size_t lds_bytes(const Args& a, int BM_, int BN_) {
   const int WN = (BN_ >= 32) ? 2 : 1, WM = 4 / WN;
   const int LDA = BM_ + 16, LDB = BN_ + ((BN_ % 32) == 0 ? 16 : 0);
-  size_t f = (size_t)BK * LDA + (size_t)BK * LDB + 2 * WM * BN_;
+  size_t f = 2 * ((size_t)BK * LDA + (size_t)BK * LDB) + 2 * WM * BN_;
   f += xf_floats(a.a.xf, a.ca_n) + xf_floats(a.b.xf, a.cb_n);
   if (a.ep.stat_mode == CV_STAT_BWD) f += 4 * (size_t)a.ce_n;
   return f * sizeof(float);
@@ -575,7 +642,7 @@ static int launch_t(const Args& a, dim3 grid, hipStream_t st) {
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)igemm_kernel<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          160 * 1024);
+                                160 * 1024);
       attr_set = true;
     }
   }
@@ -585,36 +652,38 @@ static int launch_t(const Args& a, dim3 grid, hipStream_t st) {
 }
 
 static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
-  // grid.x covers M (for SCATTER the largest class), grid.y covers N
-  const int gx = cdiv(a.M, BM_), gy = cdiv(a.N, BN_);
+  const int Ntot = a.N + ((a.op == OP_WGRAD && a.gbias) ? 1 : 0);
+  const int gx = cdiv(a.M, BM_), gy = cdiv(Ntot, BN_);
   dim3 grid(gx, gy, gz);
   CV_REQUIRE(gx > 0 && gy > 0 && gz > 0, "igemm: empty grid");
   CV_REQUIRE(gx < (1 << 30) && gy < 65536 && gz < 65536, "igemm: grid too large");
   if (BM_ == 128 && BN_ == 64) return launch_t<128, 64>(a, grid, st);
   if (BM_ == 128 && BN_ == 32) return launch_t<128, 32>(a, grid, st);
+  if (BM_ == 128 && BN_ == 16) return launch_t<128, 16>(a, grid, st);
   if (BM_ == 64 && BN_ == 64) return launch_t<64, 64>(a, grid, st);
   if (BM_ == 64 && BN_ == 32) return launch_t<64, 32>(a, grid, st);
   if (BM_ == 64 && BN_ == 16) return launch_t<64, 16>(a, grid, st);
-  if (BM_ == 128 && BN_ == 16) return launch_t<128, 16>(a, grid, st);
   cv::set_error("igemm: unsupported tile %dx%d", BM_, BN_);
   return 1;
 }
 
-static int pick_bn(int N) {
-  if (N <= 16) return 16;
-  if (N <= 32) return 32;
-  return 64;
+// Row-oriented tile: prefer 64-wide N tiles, shrink N (keeping BM=64) until there are >= 512
+// workgroups to cover the 256 CUs twice; BM=128 only for very tall problems.
+static void pick_tile(long M, int N, int& BM_, int& BN_) {
+  BN_ = (N <= 16) ? 16 : (N <= 32) ? 32 : 64;
+  BM_ = (M >= 128L * 1024) ? 128 : 64;
+  while (BN_ > 16 && (long)cdiv(M, BM_) * cdiv(N, BN_) < 512) BN_ >>= 1;
 }
 
-// number of K splits: aim for ~1024 workgroups but keep >= 256 K elements per split
+// number of K splits: aim for ~1024 workgroups but keep >= 4 K tiles per split
 static int pick_split(long tiles, long K, int requested) {
   if (requested > 0) return requested;
   long want = (1024 + tiles - 1) / tiles;
-  long maxs = K / 256;
+  long maxs = K / (4 * BK);
   if (maxs < 1) maxs = 1;
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
-  if (want > 512) want = 512;
+  if (want > 1024) want = 1024;
   return (int)want;
 }
 
@@ -626,7 +695,6 @@ static void init_args(Args& a) {
   a.ep.stat_div = 1;
   a.a_pix = 1;
   a.o_pix = 1;
-  a.ksplit = 1;
 }
 
 static int check_operand(const cv_operand* o, const char* what) {
@@ -695,9 +763,9 @@ static int check_conv(const cv_conv* g) {
   return 0;
 }
 
-// GATHER with small = rows.  `in` is the big-grid tensor.
+// GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
 static int run_gather(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
-                      int accumulate, const cv_epilogue* ep, hipStream_t st, const char* what) {
+                      const cv_epilogue* ep, hipStream_t st, const char* what) {
   Args a;
   init_args(a);
   a.op = OP_GATHER;
@@ -711,20 +779,14 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
   a.M = g.n * g.hs * g.ws;
   a.N = g.cs;
   a.K = g.kh * g.kw * g.cb;
-  a.accumulate = accumulate;
   if (apply_epilogue(a, ep, a.N, what)) return 1;
-  const int BM_ = (a.M >= 64 * 512) ? 128 : 64;
-  const int BN_ = pick_bn(a.N);
-  long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
-  int split = 1;
-  if (accumulate) split = pick_split(tiles, a.K, 0);
-  a.kchunk = ((cdiv(a.K, split) + BK - 1) / BK) * BK;
-  split = cdiv(a.K, a.kchunk);
-  a.ksplit = split;
-  return launch(a, BM_, BN_, split, st);
+  int BM_, BN_;
+  pick_tile(a.M, a.N, BM_, BN_);
+  a.kchunk = ((a.K + BK - 1) / BK) * BK;
+  return launch(a, BM_, BN_, 1, st);
 }
 
-// SCATTER with big = rows. `in` is the small-grid tensor.
+// SCATTER with big = rows. `in` is the small-grid tensor; w is packed [tap][cs][cb].
 static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                        const cv_epilogue* ep, hipStream_t st, const char* what) {
   Args a;
@@ -737,15 +799,12 @@ static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const
   a.w = w;
   a.bias = bias;
   a.out = out;
-  // largest class: ceil(hb/s) x ceil(wb/s)
-  a.M = g.n * cdiv(g.hb, g.s) * cdiv(g.wb, g.s);
+  a.M = g.n * cdiv(g.hb, g.s) * cdiv(g.wb, g.s);  // largest class
   a.N = g.cb;
   a.K = cdiv(g.kh, g.s) * cdiv(g.kw, g.s) * g.cs;
   if (apply_epilogue(a, ep, a.N, what)) return 1;
-  // every big pixel must be written exactly once: classes with no taps write bias only -> the
-  // kernel handles K == 0 by skipping the main loop.
-  const int BM_ = (a.M >= 64 * 512) ? 128 : 64;
-  const int BN_ = pick_bn(a.N);
+  int BM_, BN_;
+  pick_tile((long)a.M * g.s * g.s, a.N, BM_, BN_);
   return launch(a, BM_, BN_, g.s * g.s, st);
 }
 
@@ -761,19 +820,20 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   a.cb_n = (big->xf != CV_XF_NONE) ? g.cb : 0;
   if (small->xf != CV_XF_NONE) CV_REQUIRE(small->bn.C == g.cs, "wgrad: small-grid BN width mismatch");
   if (big->xf != CV_XF_NONE) CV_REQUIRE(big->bn.C == g.cb, "wgrad: big-grid BN width mismatch");
+  CV_REQUIRE(!small->nchw, "wgrad: the small-grid operand must be NHWC");
   a.out = gw;
   a.gbias = gbias;
   a.M = g.cs;
-  a.N = g.kh * g.kw * g.cb + (gbias ? 1 : 0);
+  a.N = g.kh * g.kw * g.cb;
+  CV_REQUIRE(!gbias || (a.N % 4) == 0, "wgrad: bias column needs taps*channels % 4 == 0");
   a.K = g.n * g.hs * g.ws;
-  a.accumulate = 1;
+  const int Ntot = a.N + (gbias ? 1 : 0);
   const int BM_ = (a.M >= 128) ? 128 : 64;
-  const int BN_ = pick_bn(a.N);
-  long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
+  const int BN_ = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
+  long tiles = (long)cdiv(a.M, BM_) * cdiv(Ntot, BN_);
   int split = pick_split(tiles, a.K, split_k);
   a.kchunk = ((cdiv(a.K, split) + BK - 1) / BK) * BK;
   split = cdiv(a.K, a.kchunk);
-  a.ksplit = split;
   return launch(a, BM_, BN_, split, st);
 }
 
@@ -781,24 +841,51 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
 
 using namespace cv;
 
-extern "C" int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* weight, const float* bias,
+extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(items && n > 0 && n <= MAX_PACK, "pack_conv_weights: 1..%d items", MAX_PACK);
+  PackArgs a;
+  memset(&a, 0, sizeof(a));
+  long mx = 0;
+  for (int i = 0; i < n; ++i) {
+    const cv_conv_pack& p = items[i];
+    CV_REQUIRE(p.src && (p.gather || p.scatter) && p.cs > 0 && p.cb > 0 && p.kh > 0 && p.kw > 0,
+               "pack_conv_weights: item %d incomplete", i);
+    a.src[i] = p.src;
+    a.dg[i] = p.gather;
+    a.ds[i] = p.scatter;
+    a.cs[i] = p.cs;
+    a.cb[i] = p.cb;
+    a.kk[i] = p.kh * p.kw;
+    const long tot = (long)p.cs * p.cb * p.kh * p.kw;
+    mx = tot > mx ? tot : mx;
+  }
+  a.n = n;
+  long gx = (mx + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(pack_kernel, dim3(gx, n), dim3(256), 0, S(stream), a);
+  CV_LAUNCH_CHECK("pack_conv_weights");
+  return 0;
+}
+
+extern "C" int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* bias,
                                float* out, const cv_epilogue* ep, cv_stream_t stream) {
   clear_error();
   if (check_conv(g) || check_operand(in, "conv_forward")) return 1;
-  CV_REQUIRE(weight && out, "conv_forward: null weight/out");
+  CV_REQUIRE(wpacked && out, "conv_forward: null weight/out");
   const Geo geo = geo_of(g);
-  if (!g->transposed) return run_gather(geo, in, weight, bias, out, 0, ep, S(stream), "conv_forward");
-  return run_scatter(geo, in, weight, bias, out, ep, S(stream), "convT_forward");
+  if (!g->transposed) return run_gather(geo, in, wpacked, bias, out, ep, S(stream), "conv_forward");
+  return run_scatter(geo, in, wpacked, bias, out, ep, S(stream), "convT_forward");
 }
 
-extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* weight, float* gin,
+extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* wpacked, float* gin,
                                      const cv_epilogue* ep, cv_stream_t stream) {
   clear_error();
   if (check_conv(g) || check_operand(gout, "conv_backward_data")) return 1;
-  CV_REQUIRE(weight && gin, "conv_backward_data: null weight/gin");
+  CV_REQUIRE(wpacked && gin, "conv_backward_data: null weight/gin");
   const Geo geo = geo_of(g);
-  if (!g->transposed) return run_scatter(geo, gout, weight, nullptr, gin, ep, S(stream), "conv_backward_data");
-  return run_gather(geo, gout, weight, nullptr, gin, 0, ep, S(stream), "convT_backward_data");
+  if (!g->transposed) return run_scatter(geo, gout, wpacked, nullptr, gin, ep, S(stream), "conv_backward_data");
+  return run_gather(geo, gout, wpacked, nullptr, gin, ep, S(stream), "convT_backward_data");
 }
 
 extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, const cv_operand* gout,
@@ -808,13 +895,23 @@ extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, c
     return 1;
   CV_REQUIRE(gweight, "conv_backward_weight: null gweight");
   const Geo geo = geo_of(g);
-  // conv: small = dY, big = X ; convT: small = X, big = dY
   CV_REQUIRE(!g->transposed || !gbias, "convT bias gradient is not a WGRAD column (use a reduction)");
+  // conv: small = dY, big = X ; convT: small = X, big = dY
   if (!g->transposed) return run_wgrad(geo, gout, in, gweight, gbias, split_k, S(stream));
   return run_wgrad(geo, in, gout, gweight, nullptr, split_k, S(stream));
 }
 
 // ---------------------------------------------------------------- linear layers
+static int linear_launch(Args& a, int accumulate, hipStream_t st) {
+  int BM_, BN_;
+  pick_tile(a.M, a.N, BM_, BN_);
+  long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
+  int split = accumulate ? pick_split(tiles, a.K, 0) : 1;
+  a.kchunk = ((cdiv(a.K, split) + BK - 1) / BK) * BK;
+  split = cdiv(a.K, a.kchunk);
+  return launch(a, BM_, BN_, split, st);
+}
+
 extern "C" int cv_linear_forward(const cv_linear* g, const cv_operand* in, const float* weight, const float* bias,
                                  float* out, int accumulate, const cv_epilogue* ep, cv_stream_t stream) {
   clear_error();
@@ -828,7 +925,6 @@ extern "C" int cv_linear_forward(const cv_linear* g, const cv_operand* in, const
   init_args(a);
   a.op = OP_DENSE;
   a.a = *in;
-  a.ca_n = 0;
   if (in->xf != CV_XF_NONE) {
     a.ca_n = in->bn.C;
     CV_REQUIRE(in->bn.C == g->in_features || (ip > 1 && in->bn.C == g->in_ch), "linear_forward: BN width mismatch");
@@ -849,12 +945,7 @@ extern "C" int cv_linear_forward(const cv_linear* g, const cv_operand* in, const
   a.o_pix = op;
   a.o_ch = g->out_ch;
   if (apply_epilogue(a, ep, a.N, "linear_forward")) return 1;
-  const int BM_ = 64, BN_ = pick_bn(a.N);
-  long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
-  int split = accumulate ? pick_split(tiles, a.K, 0) : 1;
-  a.kchunk = ((cdiv(a.K, split) + BK - 1) / BK) * BK;
-  split = cdiv(a.K, a.kchunk);
-  return launch(a, BM_, BN_, split, S(stream));
+  return linear_launch(a, accumulate, S(stream));
 }
 
 extern "C" int cv_linear_backward_data(const cv_linear* g, const cv_operand* gout, const float* weight, float* gin,
@@ -869,7 +960,6 @@ extern "C" int cv_linear_backward_data(const cv_linear* g, const cv_operand* gou
   init_args(a);
   a.op = OP_DENSE;
   a.a = *gout;
-  a.ca_n = 0;
   if (gout->xf != CV_XF_NONE) {
     a.ca_n = gout->bn.C;
     CV_REQUIRE(gout->bn.C == g->out_features, "linear_backward_data: BN width must equal out_features");
@@ -889,12 +979,7 @@ extern "C" int cv_linear_backward_data(const cv_linear* g, const cv_operand* gou
   a.o_pix = ip;
   a.o_ch = g->in_ch;
   if (apply_epilogue(a, ep, a.N, "linear_backward_data")) return 1;
-  const int BM_ = 64, BN_ = pick_bn(a.N);
-  long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
-  int split = accumulate ? pick_split(tiles, a.K, 0) : 1;
-  a.kchunk = ((cdiv(a.K, split) + BK - 1) / BK) * BK;
-  split = cdiv(a.K, a.kchunk);
-  return launch(a, BM_, BN_, split, S(stream));
+  return linear_launch(a, accumulate, S(stream));
 }
 
 extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
@@ -905,7 +990,7 @@ extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* g
   const int ip = g->in_pix > 0 ? g->in_pix : 1;
   CV_REQUIRE(g->out_pix <= 1, "linear_backward_weight: permuted outputs unsupported (use cv_declinear_*)");
   CV_REQUIRE(gout->xf == CV_XF_NONE, "linear_backward_weight: transform on gout unsupported");
-  // Expressed as a WGRAD over a 1x1 "small grid" (rows = batch) and an in_pix "big grid":
+  // a WGRAD over a 1x1 "small grid" (rows = batch) and an in_pix "big grid":
   //   dW[o][c][pix] = sum_n gout[n][o] * T(in[n][pix][c])   (== Linear weight [o][c*pix + p])
   Geo geo;
   geo.n = g->n;

@@ -116,7 +116,13 @@ class cv_mlp_grad(ctypes.Structure):
 
 _P = POINTER
 # name -> (restype, argtypes)
+class cv_conv_pack(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("gather", c_void_p), ("scatter", c_void_p),
+                ("cs", c_int), ("cb", c_int), ("kh", c_int), ("kw", c_int)]
+
+
 _SIGS = {
+    "cv_pack_conv_weights": (c_int, [_P(cv_conv_pack), c_int, c_void_p]),
     "cv_conv_forward": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_data": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_weight": (

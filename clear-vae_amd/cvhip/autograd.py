@@ -14,7 +14,7 @@ import torch
 
 from . import _lib, rng
 from ._lib import MI_CLUBSAMPLE, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
-from .plan import Program, Workspace, ensure_arena
+from .plan import Program, Workspace, ensure_arena, pack_program
 
 
 def _require_gpu(*ts):
@@ -74,6 +74,7 @@ class EncodeFn(torch.autograd.Function):
         P = Program()
         if train:
             P.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+        pack_program(sp, P, "enc")
         ws.encoder_program(P, xc, train)
         if train:
             ws.running_program(P, "enc")
@@ -130,6 +131,7 @@ class DecodeFn(torch.autograd.Function):
         P = Program()
         if train:
             P.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+        pack_program(sp, P, "dec")
         ws.decoder_program(P, zc, train, "xhat")
         if train:
             ws.running_program(P, "dec")

@@ -35,7 +35,7 @@ import torch.distributed as dist
 from . import _lib, rng
 from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
 from .autograd import est_params, mlp_struct
-from .plan import ParamArena, Program, Workspace, ensure_arena
+from .plan import ParamArena, Program, Workspace, ensure_arena, pack_program
 
 
 def _dist_world():
@@ -232,6 +232,7 @@ class ClearStep:
             f = Program()
             f.add("cv_zero", ws.stats, ws.stats.numel() * 8)
             f.add("cv_zero", A.grad, A.numel * 4)
+            pack_program(sp, f, "all")
             ws.encoder_program(f, X, True)
             ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
             ws.decoder_program(f, ws.z, True, "loss", X)
@@ -286,6 +287,7 @@ class ClearStep:
 
             def make_learn(inject: bool):
                 lp = Program()
+                pack_program(sp, lp, "all")  # the VAE Adam step just moved the weights
                 for j in range(5):
                     lp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
                     ws.encoder_program(lp, X, True)

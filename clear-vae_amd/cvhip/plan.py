@@ -31,6 +31,7 @@ from ._lib import (
     XF_NONE,
     cv_bn,
     cv_conv,
+    cv_conv_pack,
     cv_epilogue,
     cv_linear,
     cv_operand,
@@ -51,6 +52,9 @@ class ConvSpec:
     c_out: int
     h_out: int
     w_out: int
+    # GEMM-native weight copies (cv_pack_conv_weights): read by the forward / backward-data launch
+    wfwd: object = None
+    wbwd: object = None
 
     def geom(self, n: int) -> cv_conv:
         m = self.mod
@@ -226,10 +230,42 @@ def ensure_arena(vae: nn.Module, spec_fn=None):
             "clear-vae_amd runs on MI355X (ROCm device 'cuda'); move the model with .to('cuda') first"
         )
     arena = ParamArena(vae_param_order(vae, spec), dev)
+    attach_packed(spec, dev)
     vae._cv_arena = arena
     vae._cv_spec = spec
     vae._cv_workspaces = {}
     return arena
+
+
+def attach_packed(spec: VaeSpec, device):
+    """Allocate the packed conv weights (one buffer) and the cv_conv_pack descriptors.
+
+    Wg[tap][cb][cs] ("gather") serves Conv2d forward / ConvTranspose2d backward-data and
+    Ws[tap][cs][cb] ("scatter") serves Conv2d backward-data / ConvTranspose2d forward, where
+    cs, cb = weight.shape[0], weight.shape[1] (include/clearvae.h, cv_conv_pack)."""
+    convs = spec.enc + spec.dec
+    total = sum(2 * c.mod.weight.numel() for c in convs)
+    buf = torch.empty(total, dtype=torch.float32, device=device)
+    o = 0
+    spec.pack_items = {"enc": [], "dec": []}
+    for part, lst in (("enc", spec.enc), ("dec", spec.dec)):
+        for c in lst:
+            w = c.mod.weight
+            k = w.numel()
+            gat, sca = buf[o:o + k], buf[o + k:o + 2 * k]
+            o += 2 * k
+            c.wfwd, c.wbwd = (sca, gat) if c.transposed else (gat, sca)
+            spec.pack_items[part].append(
+                cv_conv_pack(w.data_ptr(), gat.data_ptr(), sca.data_ptr(), w.shape[0], w.shape[1], w.shape[2],
+                             w.shape[3]))
+    spec.packed = buf
+
+
+def pack_program(spec: VaeSpec, P: "Program", which: str = "all"):
+    """Refresh the packed conv weights from the (arena) parameters: one launch."""
+    items = spec.pack_items["enc"] * (which != "dec") + spec.pack_items["dec"] * (which != "enc")
+    if items:
+        P.add("cv_pack_conv_weights", struct_array(cv_conv_pack, items), len(items))
 
 
 # ----------------------------------------------------------------------------- BN plumbing
@@ -406,7 +442,7 @@ class Workspace:
             else:
                 op = operand(cur, XF_BNRELU, self.bn_enc[li - 1].cv(train))
             ep = ep_fwd(self.bn_enc[li]) if train else ep_none()
-            P.add("cv_conv_forward", g, op, c.mod.weight, c.mod.bias, self.y_enc[li], ep)
+            P.add("cv_conv_forward", g, op, c.wfwd, c.mod.bias, self.y_enc[li], ep)
             cur = self.y_enc[li]
         # heads (Linear on the NCHW-flattened activation), split-K into a zeroed buffer
         C, Hh, Wh = sp.feat
@@ -437,7 +473,7 @@ class Workspace:
             g = c.geom(n)
             op = operand(cur) if li == 0 else operand(cur, XF_BNRELU, self.bn_dec[li - 1].cv(train))
             ep = ep_fwd(self.bn_dec[li]) if train else ep_none()
-            P.add("cv_conv_forward", g, op, c.mod.weight, c.mod.bias, self.y_dec[li], ep)
+            P.add("cv_conv_forward", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep)
             cur = self.y_dec[li]
         last = sp.dec[-1]
         hw = last.h_out * last.w_out
@@ -459,10 +495,10 @@ class Workspace:
             gout = operand(self.g_dec[li], XF_BNBWD, self.bn_dec[li].cv(True), y=self.y_dec[li])
             if li > 0:
                 ep = ep_bwd(self.bn_dec[li - 1], self.y_dec[li - 1], sp.dec[li - 1].relu)
-                P.add("cv_conv_backward_data", g, gout, c.mod.weight, self.g_dec[li - 1], ep)
+                P.add("cv_conv_backward_data", g, gout, c.wbwd, self.g_dec[li - 1], ep)
                 xin = operand(self.y_dec[li - 1], XF_BNRELU, self.bn_dec[li - 1].cv(True))
             else:
-                P.add("cv_conv_backward_data", g, gout, c.mod.weight, self.gah, ep_none())
+                P.add("cv_conv_backward_data", g, gout, c.wbwd, self.gah, ep_none())
                 xin = operand(self.ah)
             P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0)
         Cu, Hu, Wu = sp.unflat
@@ -489,11 +525,11 @@ class Workspace:
             gout = operand(self.g_enc[li], XF_BNBWD, self.bn_enc[li].cv(True), y=self.y_enc[li])
             if li > 0:
                 ep = ep_bwd(self.bn_enc[li - 1], self.y_enc[li - 1], True)
-                P.add("cv_conv_backward_data", g, gout, c.mod.weight, self.g_enc[li - 1], ep)
+                P.add("cv_conv_backward_data", g, gout, c.wbwd, self.g_enc[li - 1], ep)
                 xin = operand(self.y_enc[li - 1], XF_BNRELU, self.bn_enc[li - 1].cv(True))
             else:
                 if dx is not None:
-                    P.add("cv_conv_backward_data", g, gout, c.mod.weight, dx, ep_none())
+                    P.add("cv_conv_backward_data", g, gout, c.wbwd, dx, ep_none())
                 xin = operand(x, nchw=1)
             P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0)
 

@@ -83,14 +83,27 @@ typedef struct cv_conv {
   int transposed;                 /* 0 Conv2d, 1 ConvTranspose2d                   */
 } cv_conv;
 
+/* GEMM-native copies of a conv / convT weight, refreshed once per optimizer step.  With
+ * w(cs, cb, tap) = W[cs][cb][kh][kw] (PyTorch layout; cs = out channels for Conv2d, in channels for
+ * ConvTranspose2d): gather = Wg[tap][cb][cs], scatter = Ws[tap][cs][cb].  Conv2d forward and
+ * ConvTranspose2d backward-data read `gather`; Conv2d backward-data and ConvTranspose2d forward read
+ * `scatter`.  Up to 16 weights per call (one launch). */
+typedef struct cv_conv_pack {
+  const float* src; float* gather; float* scatter;
+  int cs, cb, kh, kw;
+} cv_conv_pack;
+int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream);
+
 /* y = conv(T(x)) + bias.  Replaces nn.Conv2d/ConvTranspose2d.forward (vae.py:15-46) with the
  * preceding BatchNorm2d+ReLU fused into the operand load and the following BatchNorm2d's batch
- * statistics fused into the epilogue. */
-int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* weight, const float* bias,
+ * statistics fused into the epilogue.  wpacked: the `gather` (Conv2d) or `scatter`
+ * (ConvTranspose2d) packing of cv_pack_conv_weights. */
+int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* bias,
                     float* out, const cv_epilogue* ep, cv_stream_t stream);
 
-/* dx = conv^T(T(dy)).  Replaces the grad_input half of aten::convolution_backward. */
-int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* weight,
+/* dx = conv^T(T(dy)).  Replaces the grad_input half of aten::convolution_backward.
+ * wpacked: `scatter` (Conv2d) or `gather` (ConvTranspose2d) packing. */
+int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* wpacked,
                           float* gin, const cv_epilogue* ep, cv_stream_t stream);
 
 /* dw += sum_pixels T(x) (x) T(dy).  Replaces the grad_weight half of aten::convolution_backward.
@@ -119,9 +132,9 @@ int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const 
 
 /* Decoder Linear -> BatchNorm1d -> ReLU backward (vae.py:33-35).  da: gradient w.r.t. the ReLU
  * output in the Unflatten/NHWC order (g->out_pix, g->out_ch); h: the Linear output (BN1d input),
- * same order.  The kernel masks da in place (da <- dz), writes the BN1d backward sums into
- * gstat_out (replica 0; other replicas must be zero) and the Linear weight gradient
- * dW[f][k] = sum_n BNbwd(dz)[n][f] * zin[n][k] (overwrite, no accumulation). */
+ * same order.  Two launches: (1) mask da in place (da <- dz) and accumulate the BN1d backward sums
+ * into gstat_out (fp64, replicas; caller zeroes); (2) accumulate the Linear weight gradient
+ * dW[f][k] += sum_n BNbwd(dz)[n][f] * zin[n][k] (caller zeroes). */
 int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, const cv_bn* bn,
                                  double* gstat_out, const float* zin, float* gweight,
                                  cv_stream_t stream);

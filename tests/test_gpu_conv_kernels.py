@@ -72,6 +72,20 @@ def _host_bnbwd(dz, y, gamma, C):
     return dy.reshape(y.shape)
 
 
+def _packed(lib_mod, W, tr):
+    """(forward, backward-data) GEMM-native weight copies via cv_pack_conv_weights."""
+    cs, cb, kh, kw = W.shape
+    gat, sca = torch.empty_like(W), torch.empty_like(W)
+    item = lib_mod.cv_conv_pack(W.data_ptr(), gat.data_ptr(), sca.data_ptr(), cs, cb, kh, kw)
+    lib_mod.call("cv_pack_conv_weights", (lib_mod.cv_conv_pack * 1)(item), 1, lib_mod.stream_handle())
+    torch.cuda.synchronize()
+    # layout contract (include/clearvae.h): Wg[tap][cb][cs], Ws[tap][cs][cb]
+    Wc = W.cpu()
+    assert torch.equal(gat.cpu().view(kh, kw, cb, cs), Wc.permute(2, 3, 1, 0))
+    assert torch.equal(sca.cpu().view(kh, kw, cs, cb), Wc.permute(2, 3, 0, 1))
+    return (sca, gat) if tr else (gat, sca)
+
+
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "T" * g[1] + f"{g[2]}x{g[3]}-{g[4]}x{g[5]}k{g[6]}")
 @pytest.mark.parametrize("xf", ["none", "bn"])
 def test_conv_fwd_bwd_wgrad(geom, xf):
@@ -92,6 +106,7 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
     rm_o, rv_o = torch.zeros(cout, device=dev), torch.ones(cout, device=dev)
     use_bn = xf == "bn" and cin % 1 == 0 and not (cin == 1 or cin == 3)
     s_ = _lib.stream_handle()
+    Wf, Wb = _packed(_lib, W, tr)
     # ---------------- forward
     if use_bn:
         gi, bi = _bn_state(cin, n * hin * hin, rng, dev)
@@ -107,7 +122,7 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
     ep.stat_mode, ep.stat_div = _lib.STAT_FWD, 1
     st_out = torch.zeros(REPL, 2, cout, dtype=torch.float64, device=dev)
     ep.stat_out = st_out.data_ptr()
-    _lib.call("cv_conv_forward", g, opnd, W.data_ptr(), b.data_ptr(), out.data_ptr(), ep, s_)
+    _lib.call("cv_conv_forward", g, opnd, Wf.data_ptr(), b.data_ptr(), out.data_ptr(), ep, s_)
     xin_nchw = xin_host.permute(0, 3, 1, 2).cpu()
     Wd, bd = W.double().cpu(), b.double().cpu()
     if tr:
@@ -137,7 +152,7 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
         gop = _lib.cv_operand(dyo.data_ptr(), None, _lib.XF_NONE, 0)
         dy_host = dyo.double()
     gin = torch.empty(n, hin, hin, cin, dtype=torch.float32, device=dev)
-    _lib.call("cv_conv_backward_data", g, gop, W.data_ptr(), gin.data_ptr(), _lib.cv_epilogue(), s_)
+    _lib.call("cv_conv_backward_data", g, gop, Wb.data_ptr(), gin.data_ptr(), _lib.cv_epilogue(), s_)
     dy_nchw = dy_host.permute(0, 3, 1, 2).cpu()
     if tr:
         gref = F.conv2d(dy_nchw, Wd, None, stride=s, padding=p)
@@ -185,7 +200,8 @@ def test_backward_data_stat_epilogue(geom):
     ep.erelu = 1
     gin = torch.empty(n, hin, hin, cin, dtype=torch.float32, device=dev)
     gop = _lib.cv_operand(dyo.data_ptr(), None, _lib.XF_NONE, 0)
-    _lib.call("cv_conv_backward_data", g, gop, W.data_ptr(), gin.data_ptr(), ep, _lib.stream_handle())
+    _, Wb = _packed(_lib, W, tr)
+    _lib.call("cv_conv_backward_data", g, gop, Wb.data_ptr(), gin.data_ptr(), ep, _lib.stream_handle())
     Wd = W.double().cpu()
     dy_nchw = dyo.double().permute(0, 3, 1, 2).cpu()
     if tr:
