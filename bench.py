@@ -199,6 +199,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-pass", action="store_true")
+    ap.add_argument("--kernel-table", default=None, help="write the per-call timing table to this file")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -272,6 +273,14 @@ def main():
                     "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None,
                     "kernel_ms": round(ms, 5), "flops_per_launch": fl}
         step_ms_eager = sum(km.values())
+        if args.kernel_table and rank == 0:
+            with open(args.kernel_table, "w") as fh:
+                fh.write(f"{'call':60s} {'ms':>9s} {'GFLOP':>9s} {'TF/s':>8s}\n")
+                for label, ms in sorted(km.items(), key=lambda kv: -kv[1]):
+                    fl = gemm_flops_of(label, G, eng)
+                    fh.write(f"{label:60s} {ms:9.4f} {(fl or 0) / 1e9:9.3f} "
+                             f"{(fl or 0) / (ms * 1e-3) / 1e12:8.2f}\n")
+                fh.write(f"{'total':60s} {step_ms_eager:9.4f}\n")
     else:
         step_ms_eager = None
 

@@ -19,29 +19,25 @@ struct RunArgs {
   float momentum;
 };
 
+// one block per layer; replica folds spread over the block for narrow layers
 __global__ __launch_bounds__(256) void bn_running_kernel(const RunArgs a) {
+  __shared__ double scratch[4 * 256];
   const int l = blockIdx.y;
   if (l >= a.nl) return;
   const cv_bn& b = a.bn[l];
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c == 0 && a.nbt[l]) a.nbt[l][0] += 1;
-  if (c >= b.C) return;
-  double s = 0.0, q = 0.0;
-#pragma unroll
-  for (int r = 0; r < CV_STAT_REPL; ++r) {
-    s += b.stat[(size_t)r * 2 * b.C + c];
-    q += b.stat[(size_t)r * 2 * b.C + b.C + c];
-  }
-  const double n = (double)b.count;
-  const double mean = s / n;
-  double var = q / n - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const double unbiased = (b.count > 1) ? var * n / (n - 1.0) : var;
+  if (threadIdx.x == 0 && a.nbt[l]) a.nbt[l][0] += 1;
   float* rm = const_cast<float*>(b.running_mean);
   float* rv = const_cast<float*>(b.running_var);
   const float m = a.momentum;
-  rm[c] = m * (float)mean + (1.0f - m) * rm[c];
-  rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
+  bn_fold<256>(b, false, scratch, [&](int c, double s, double q, double, double) {
+    const double n = (double)b.count;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const double unbiased = (b.count > 1) ? var * n / (n - 1.0) : var;
+    rm[c] = m * (float)mean + (1.0f - m) * rm[c];
+    rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
+  });
 }
 
 struct GradArgs {
@@ -51,19 +47,17 @@ struct GradArgs {
   int nl;
 };
 __global__ __launch_bounds__(256) void bn_grads_kernel(const GradArgs a) {
+  __shared__ double scratch[4 * 256];
   const int l = blockIdx.y;
   if (l >= a.nl) return;
-  const cv_bn& b = a.bn[l];
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= b.C) return;
-  double s = 0.0, q = 0.0;
-#pragma unroll
-  for (int r = 0; r < CV_STAT_REPL; ++r) {
-    s += b.gstat[(size_t)r * 2 * b.C + c];
-    q += b.gstat[(size_t)r * 2 * b.C + b.C + c];
-  }
-  if (a.db[l]) a.db[l][c] = (float)s;
-  if (a.dg[l]) a.dg[l][c] = (float)q;
+  cv_bn b = a.bn[l];
+  b.stat = b.gstat;  // fold the backward sums
+  float* dg = a.dg[l];
+  float* db = a.db[l];
+  bn_fold<256>(b, false, scratch, [&](int c, double s, double q, double, double) {
+    if (db) db[c] = (float)s;
+    if (dg) dg[c] = (float)q;
+  });
 }
 
 __global__ void bn_stats_kernel(const cv_bn b, float* mean, float* invstd) {
@@ -82,8 +76,8 @@ constexpr int OUT_MAXC = 4;
 __global__ __launch_bounds__(256) void output_fwd_kernel(const cv_bn b, const float* __restrict__ y, int n, int c,
                                                          int hw, float* __restrict__ xhat) {
   __shared__ BnFwdC k[OUT_MAXC];
-  if (threadIdx.x < c) k[threadIdx.x] = bn_fwd_const(b, threadIdx.x);
-  __syncthreads();
+  __shared__ double scratch[4 * 256];
+  bn_fold<256>(b, false, scratch, [&](int f, double s, double q, double, double) { k[f] = bn_fwd_const_s(b, f, s, q); });
   const long total = (long)n * c * hw;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int p = (int)(i % hw);
@@ -105,13 +99,11 @@ __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const f
   __shared__ BnFwdC k[OUT_MAXC];
   __shared__ float2 mi[OUT_MAXC];
   __shared__ double red[4][1 + 2 * OUT_MAXC];
-  if (threadIdx.x < c) {
-    k[threadIdx.x] = bn_fwd_const(b, threadIdx.x);
-    float m_, i_;
-    bn_mean_istd(b, threadIdx.x, m_, i_);
-    mi[threadIdx.x] = make_float2(m_, i_);
-  }
-  __syncthreads();
+  __shared__ double scratch[4 * 256];
+  bn_fold<256>(b, false, scratch, [&](int f, double s, double q, double, double) {
+    k[f] = bn_fwd_const_s(b, f, s, q);
+    mi[f] = make_float2(k[f].mu, k[f].istd);
+  });
   const float scale = (rec_scale ? rec_scale[0] : 1.0f) * 2.0f / (float)n;
   const long total = (long)n * c * hw;
   float rec = 0.f;
@@ -157,7 +149,7 @@ __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const f
     double r = red[0][0] + red[1][0] + red[2][0] + red[3][0];
     atomic_add_f64(rec_out, r / (double)n);
     if (dv) {
-      const int repl = blockIdx.x % CV_STAT_REPL;
+      const int repl = blockIdx.x % CV_STAT_REPL(c);
       for (int j = 0; j < c; ++j) {
         const double a = red[0][1 + j] + red[1][1 + j] + red[2][1 + j] + red[3][1 + j];
         const double bb = red[0][1 + OUT_MAXC + j] + red[1][1 + OUT_MAXC + j] + red[2][1 + OUT_MAXC + j] +
@@ -175,12 +167,12 @@ __global__ __launch_bounds__(256) void output_bwd_kernel(const cv_bn b, const fl
                                                          float* __restrict__ dv, double* gstat) {
   __shared__ float2 mi[OUT_MAXC];
   __shared__ double red[4][2 * OUT_MAXC];
-  if (threadIdx.x < c) {
+  __shared__ double scratch[4 * 256];
+  bn_fold<256>(b, false, scratch, [&](int f, double s, double q, double, double) {
     float m_, i_;
-    bn_mean_istd(b, threadIdx.x, m_, i_);
-    mi[threadIdx.x] = make_float2(m_, i_);
-  }
-  __syncthreads();
+    bn_mean_istd_s(b, f, s, q, m_, i_);
+    mi[f] = make_float2(m_, i_);
+  });
   const long total = (long)n * c * hw;
   float s1[OUT_MAXC], s2[OUT_MAXC];
 #pragma unroll
@@ -209,7 +201,7 @@ __global__ __launch_bounds__(256) void output_bwd_kernel(const cv_bn b, const fl
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int repl = blockIdx.x % CV_STAT_REPL;
+    const int repl = blockIdx.x % CV_STAT_REPL(c);
     for (int j = 0; j < c; ++j) {
       atomic_add_f64(gstat + (size_t)repl * 2 * c + j, red[0][j] + red[1][j] + red[2][j] + red[3][j]);
       atomic_add_f64(gstat + (size_t)repl * 2 * c + c + j,
@@ -280,7 +272,7 @@ __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int p
   if (t < DL_F && f0 + t < F) {
     const double a = (double)r1[0][t] + r1[1][t] + r1[2][t] + r1[3][t];
     const double q = (double)r2[0][t] + r2[1][t] + r2[2][t] + r2[3][t];
-    const int repl = blockIdx.y % CV_STAT_REPL;
+    const int repl = (blockIdx.y * gridDim.x + blockIdx.x) % CV_STAT_REPL(F);
     atomic_add_f64(gstat + (size_t)repl * 2 * F + f0 + t, a);
     atomic_add_f64(gstat + (size_t)repl * 2 * F + F + f0 + t, q);
   }
@@ -354,7 +346,7 @@ extern "C" int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum
   }
   a.nl = nlayers;
   a.momentum = momentum;
-  hipLaunchKernelGGL(bn_running_kernel, dim3(cdiv(cmax, 256), nlayers), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(bn_running_kernel, dim3(1, nlayers), dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("bn_update_running");
   return 0;
 }
@@ -385,7 +377,7 @@ extern "C" int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dga
     cmax = bn[i].C > cmax ? bn[i].C : cmax;
   }
   a.nl = nlayers;
-  hipLaunchKernelGGL(bn_grads_kernel, dim3(cdiv(cmax, 256), nlayers), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(bn_grads_kernel, dim3(1, nlayers), dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("bn_param_grads");
   return 0;
 }

@@ -71,14 +71,9 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 struct BnFwdC { float sc, mu, be, istd; };      // a = max((x - mu)*sc + be, 0), sc = gamma*istd
 struct BnBwdC { float sc, mu, istd, c1, c2; };   // dy = sc*(dz - c1 - (y-mu)*istd*c2)
 
-__device__ __forceinline__ void bn_mean_istd(const cv_bn& b, int c, float& mean, float& istd) {
+// mean / istd of feature c from its (replica-folded) fp64 sums (train) or the running stats (eval)
+__device__ __forceinline__ void bn_mean_istd_s(const cv_bn& b, int c, double s, double q, float& mean, float& istd) {
   if (b.train) {
-    double s = 0.0, q = 0.0;
-#pragma unroll
-    for (int r = 0; r < CV_STAT_REPL; ++r) {
-      s += b.stat[(size_t)r * 2 * b.C + c];
-      q += b.stat[(size_t)r * 2 * b.C + b.C + c];
-    }
     const double inv_n = 1.0 / (double)b.count;
     const double m = s * inv_n;
     double var = q * inv_n - m * m;
@@ -91,9 +86,9 @@ __device__ __forceinline__ void bn_mean_istd(const cv_bn& b, int c, float& mean,
   }
 }
 
-__device__ __forceinline__ BnFwdC bn_fwd_const(const cv_bn& b, int c) {
+__device__ __forceinline__ BnFwdC bn_fwd_const_s(const cv_bn& b, int c, double s, double q) {
   float mean, istd;
-  bn_mean_istd(b, c, mean, istd);
+  bn_mean_istd_s(b, c, s, q, mean, istd);
   const float g = b.gamma ? b.gamma[c] : 1.f, be = b.beta ? b.beta[c] : 0.f;
   BnFwdC r;
   r.sc = g * istd;
@@ -103,28 +98,101 @@ __device__ __forceinline__ BnFwdC bn_fwd_const(const cv_bn& b, int c) {
   return r;
 }
 
-__device__ __forceinline__ BnBwdC bn_bwd_const(const cv_bn& b, int c) {
+__device__ __forceinline__ BnBwdC bn_bwd_const_s(const cv_bn& b, int c, double s, double q, double gs, double gq) {
   float mean, istd;
-  bn_mean_istd(b, c, mean, istd);
+  bn_mean_istd_s(b, c, s, q, mean, istd);
   const float g = b.gamma ? b.gamma[c] : 1.f;
   BnBwdC r;
   r.sc = g * istd;
   r.mu = mean;
   r.istd = istd;
-  if (b.train) {
-    double s = 0.0, q = 0.0;
-#pragma unroll
-    for (int rr = 0; rr < CV_STAT_REPL; ++rr) {
-      s += b.gstat[(size_t)rr * 2 * b.C + c];
-      q += b.gstat[(size_t)rr * 2 * b.C + b.C + c];
-    }
-    r.c1 = (float)(s / (double)b.count);
-    r.c2 = (float)(q / (double)b.count);
-  } else {
-    r.c1 = 0.f;
-    r.c2 = 0.f;
-  }
+  r.c1 = b.train ? (float)(gs / (double)b.count) : 0.f;
+  r.c2 = b.train ? (float)(gq / (double)b.count) : 0.f;
   return r;
+}
+
+// serial replica fold of one feature (a single thread; fine for wide layers, R <= 16)
+__device__ __forceinline__ void bn_sums(const double* st, int C, int c, double& s, double& q) {
+  s = 0.0;
+  q = 0.0;
+  if (!st) return;
+  for (int r = 0, R = CV_STAT_REPL(C); r < R; ++r) {
+    s += st[(size_t)r * 2 * C + c];
+    q += st[(size_t)r * 2 * C + C + c];
+  }
+}
+
+__device__ __forceinline__ void bn_mean_istd(const cv_bn& b, int c, float& mean, float& istd) {
+  double s = 0.0, q = 0.0;
+  if (b.train) bn_sums(b.stat, b.C, c, s, q);
+  bn_mean_istd_s(b, c, s, q, mean, istd);
+}
+
+__device__ __forceinline__ BnFwdC bn_fwd_const(const cv_bn& b, int c) {
+  double s = 0.0, q = 0.0;
+  if (b.train) bn_sums(b.stat, b.C, c, s, q);
+  return bn_fwd_const_s(b, c, s, q);
+}
+
+__device__ __forceinline__ BnBwdC bn_bwd_const(const cv_bn& b, int c) {
+  double s = 0.0, q = 0.0, gs = 0.0, gq = 0.0;
+  if (b.train) {
+    bn_sums(b.stat, b.C, c, s, q);
+    bn_sums(b.gstat, b.C, c, gs, gq);
+  }
+  return bn_bwd_const_s(b, c, s, q, gs, gq);
+}
+
+// Block-cooperative replica fold: calls fn(f, s, q, gs, gq) once per feature f < b.C with the
+// replica-summed fp64 sums (zeros in eval mode).  Narrow layers (many replicas) spread each
+// feature's replicas over G threads and combine the partials through `scratch` (>= 4*NT doubles of
+// LDS that is not live yet).  Every thread of the block must call it; it ends with a barrier.
+template <int NT, typename Fn>
+__device__ __forceinline__ void bn_fold(const cv_bn& b, bool with_g, double* scratch, Fn fn) {
+  const int C = b.C, t = threadIdx.x;
+  const int R = CV_STAT_REPL(C);
+  int G = 1;
+  if (b.train)
+    while (2 * G * C <= NT && 2 * G <= R) G *= 2;
+  if (G == 1) {
+    for (int f = t; f < C; f += NT) {
+      double s = 0.0, q = 0.0, gs = 0.0, gq = 0.0;
+      if (b.train) {
+        bn_sums(b.stat, C, f, s, q);
+        if (with_g) bn_sums(b.gstat, C, f, gs, gq);
+      }
+      fn(f, s, q, gs, gq);
+    }
+  } else {
+    const int f = t / G, j = t - f * G;
+    double s = 0.0, q = 0.0, gs = 0.0, gq = 0.0;
+    if (f < C) {
+      for (int r = j; r < R; r += G) {
+        s += b.stat[(size_t)r * 2 * C + f];
+        q += b.stat[(size_t)r * 2 * C + C + f];
+        if (with_g) {
+          gs += b.gstat[(size_t)r * 2 * C + f];
+          gq += b.gstat[(size_t)r * 2 * C + C + f];
+        }
+      }
+    }
+    scratch[t] = s;
+    scratch[NT + t] = q;
+    scratch[2 * NT + t] = gs;
+    scratch[3 * NT + t] = gq;
+    __syncthreads();
+    if (t < C) {
+      double a = 0.0, bq = 0.0, c = 0.0, d = 0.0;
+      for (int i = 0; i < G; ++i) {
+        a += scratch[t * G + i];
+        bq += scratch[NT + t * G + i];
+        c += scratch[2 * NT + t * G + i];
+        d += scratch[3 * NT + t * G + i];
+      }
+      fn(t, a, bq, c, d);
+    }
+  }
+  __syncthreads();
 }
 
 // (x - mu) first: the subtraction is exact for x near mu, so the sign test of a near-zero BN output

@@ -46,6 +46,7 @@ struct Args {
   int ldb;
   const float* bias;
   float* gbias;        // WGRAD: bias gradient via an extra all-ones B column
+  float* part;         // WGRAD split-K: partial tiles [split][M][N(+1)] (else fp32 atomics)
   float* out;
   int accumulate;      // atomicAdd into out (split-K)
   cv_epilogue ep;
@@ -79,15 +80,20 @@ __device__ __forceinline__ float4 xf_apply4(const cv_operand& o, const XfA& c, i
   return v;
 }
 
-__device__ __forceinline__ void fill_consts(const cv_operand& o, int nfeat, float* lds, XfA& c) {
+// BN constants of an operand into LDS (block-cooperative replica fold; scratch: 4*NT doubles)
+__device__ __forceinline__ void fill_consts(const cv_operand& o, int nfeat, float* lds, double* scratch, XfA& c) {
   c.f = reinterpret_cast<const BnFwdC*>(lds);
   c.bw = reinterpret_cast<const BnBwdC*>(lds);
   if (o.xf == CV_XF_BNRELU) {
     BnFwdC* d = reinterpret_cast<BnFwdC*>(lds);
-    for (int i = threadIdx.x; i < nfeat; i += NT) d[i] = bn_fwd_const(o.bn, i);
+    bn_fold<NT>(o.bn, false, scratch, [&](int f, double s, double q, double, double) {
+      if (f < nfeat) d[f] = bn_fwd_const_s(o.bn, f, s, q);
+    });
   } else if (o.xf == CV_XF_BNBWD) {
     BnBwdC* d = reinterpret_cast<BnBwdC*>(lds);
-    for (int i = threadIdx.x; i < nfeat; i += NT) d[i] = bn_bwd_const(o.bn, i);
+    bn_fold<NT>(o.bn, true, scratch, [&](int f, double s, double q, double gs, double gq) {
+      if (f < nfeat) d[f] = bn_bwd_const_s(o.bn, f, s, q, gs, gq);
+    });
   }
 }
 
@@ -155,12 +161,17 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   }
 
   // ---------------- prologue: BN constants into LDS
+  // (the A tile buffers are not live yet: they serve as the fold's scratch)
+  double* fold_scratch = reinterpret_cast<double*>(As);
+  static_assert(2 * BK * LDA * sizeof(float) >= 4 * NT * sizeof(double), "fold scratch");
   XfA ca, cb;
-  fill_consts(P.a, P.ca_n, cstA, ca);
-  fill_consts(P.b, P.cb_n, cstB, cb);
+  fill_consts(P.a, P.ca_n, cstA, fold_scratch, ca);
+  fill_consts(P.b, P.cb_n, cstB, fold_scratch, cb);
   if (P.ep.stat_mode == CV_STAT_BWD) {
     BnFwdC* d = reinterpret_cast<BnFwdC*>(cstE);
-    for (int i = t; i < P.ce_n; i += NT) d[i] = bn_fwd_const(P.ep.ebn, i);
+    bn_fold<NT>(P.ep.ebn, false, fold_scratch, [&](int f, double s, double q, double, double) {
+      if (f < P.ce_n) d[f] = bn_fwd_const_s(P.ep.ebn, f, s, q);
+    });
   }
 
   // ---------------- per-thread A-row decode (row-oriented problems): rows (t&15)+16*(t>>7)+32*i,
@@ -499,7 +510,6 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
 
   // ---------------- epilogue
   const bool stats = P.ep.stat_mode != CV_STAT_NONE;
-  const int repl = blockIdx.x % CV_STAT_REPL;
   float s1[FN], s2[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
@@ -515,13 +525,15 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
         float v = acc[i][j][r];
         if (row >= M || col >= N) continue;
         if (op == OP_WGRAD) {
-          if (col >= P.N) {  // bias column
-            atomicAdd(P.gbias + row, v);
+          if (P.part) {  // plain store of this split's partial tile; wgrad_reduce_kernel sums them
+            P.part[((size_t)blockIdx.z * M + row) * N + col] = v;
             continue;
           }
           const Geo& g = P.g;
           const int tap = col / g.cb, c = col - tap * g.cb;  // w layout [cs][cb][kh][kw]
-          atomicAdd(P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap, v);
+          float* dst = (col >= P.N) ? P.gbias + row : P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap;
+          if (gridDim.z == 1) *dst += v;  // single writer
+          else atomicAdd(dst, v);
           continue;
         }
         size_t off;
@@ -590,6 +602,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
         }
         const int f = col / P.ep.stat_div;
         const int C = (P.ep.stat_mode == CV_STAT_BWD) ? P.ce_n : P.ep.ebn.C;
+        const int repl = (blockIdx.x + blockIdx.z * gridDim.x) % CV_STAT_REPL(C);
         double* so = P.ep.stat_out + (size_t)repl * 2 * C;
         atomic_add_f64(so + f, a);
         atomic_add_f64(so + C + f, b);
@@ -621,6 +634,33 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
     const float v = a.src[l][i];
     if (a.dg[l]) a.dg[l][((size_t)tap * cbn + c_b) * cs + c_s] = v;
     if (a.ds[l]) a.ds[l][((size_t)tap * cs + c_s) * cbn + c_b] = v;
+  }
+}
+
+// ------------------------------------------------------------------ split-K reduction of WGRAD
+// gw[row][c][tap] += sum_s part[s][row][tap*cb + c]; gbias[row] += sum_s part[s][row][N]
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int split, int M, int N,
+                                                           int ntot, int cb, int kk, float* gw, float* gbias) {
+  const long total = (long)M * N + (gbias ? M : 0);
+  const size_t sstride = (size_t)M * ntot;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int row, col;
+    float* dst;
+    if (i < (long)M * N) {
+      row = (int)(i / N);
+      const int rem = (int)(i - (long)row * N);
+      const int c = rem / kk, tap = rem - c * kk;
+      col = tap * cb + c;
+      dst = gw + i;
+    } else {
+      row = (int)(i - (long)M * N);
+      col = N;
+      dst = gbias + row;
+    }
+    const float* p = part + (size_t)row * ntot + col;
+    float acc = 0.f;
+    for (int z = 0; z < split; ++z) acc += p[z * sstride];
+    *dst += acc;
   }
 }
 
@@ -808,8 +848,44 @@ static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const
   return launch(a, BM_, BN_, g.s * g.s, st);
 }
 
+struct WPlan {
+  int BM, BN, split, kchunk;
+};
+
+// Split-K plan of a WGRAD problem (independent of whether a bias column is present, so the
+// workspace query and the launch agree): ~1024 workgroups, >= 8 K tiles per split (>= 4 when the
+// problem would otherwise not fill the 256 CUs).
+static WPlan wgrad_plan(int M, int N, long K, int split_k) {
+  WPlan w;
+  const int Ntot = N + 1;
+  w.BM = (M >= 128) ? 128 : 64;
+  w.BN = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
+  const long tiles = (long)cdiv(M, w.BM) * cdiv(Ntot, w.BN);
+  const long ktiles = (K + BK - 1) / BK;
+  long split;
+  if (split_k > 0) {
+    split = split_k;
+  } else {
+    split = (1024 + tiles - 1) / tiles;
+    long maxs = ktiles / 8;
+    if (tiles * maxs < 256) maxs = ktiles / 4;
+    if (maxs < 1) maxs = 1;
+    if (split > maxs) split = maxs;
+    if (split < 1) split = 1;
+  }
+  if (split > 4096) split = 4096;
+  w.kchunk = (int)(((K + split - 1) / split + BK - 1) / BK) * BK;
+  w.split = (int)((K + w.kchunk - 1) / w.kchunk);
+  return w;
+}
+
+static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
+  const WPlan w = wgrad_plan(M, N, K, split_k);
+  return w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
+}
+
 static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias,
-                     int split_k, hipStream_t st) {
+                     int split_k, float* work, size_t work_bytes, hipStream_t st) {
   Args a;
   init_args(a);
   a.op = OP_WGRAD;
@@ -827,14 +903,24 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   a.N = g.kh * g.kw * g.cb;
   CV_REQUIRE(!gbias || (a.N % 4) == 0, "wgrad: bias column needs taps*channels % 4 == 0");
   a.K = g.n * g.hs * g.ws;
+  const WPlan w = wgrad_plan(a.M, a.N, a.K, split_k);
+  a.kchunk = w.kchunk;
   const int Ntot = a.N + (gbias ? 1 : 0);
-  const int BM_ = (a.M >= 128) ? 128 : 64;
-  const int BN_ = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
-  long tiles = (long)cdiv(a.M, BM_) * cdiv(Ntot, BN_);
-  int split = pick_split(tiles, a.K, split_k);
-  a.kchunk = ((cdiv(a.K, split) + BK - 1) / BK) * BK;
-  split = cdiv(a.K, a.kchunk);
-  return launch(a, BM_, BN_, split, st);
+  if (w.split > 1 && work) {
+    const size_t need = (size_t)w.split * a.M * Ntot * sizeof(float);
+    CV_REQUIRE(work_bytes >= need, "wgrad: workspace %zu bytes < %zu needed", work_bytes, need);
+    a.part = work;
+  }
+  if (launch(a, w.BM, w.BN, w.split, st)) return 1;
+  if (a.part) {
+    const long total = (long)a.M * a.N + (gbias ? a.M : 0);
+    long blocks = (total + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, work, w.split, a.M, a.N, Ntot, g.cb,
+                       g.kh * g.kw, gw, gbias);
+    CV_LAUNCH_CHECK("wgrad_reduce");
+  }
+  return 0;
 }
 
 }  // namespace cv
@@ -888,8 +974,15 @@ extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, c
   return run_gather(geo, gout, wpacked, nullptr, gin, ep, S(stream), "convT_backward_data");
 }
 
+extern "C" size_t cv_conv_wgrad_workspace_bytes(const cv_conv* g, int split_k) {
+  if (!g) return 0;
+  const Geo geo = geo_of(g);
+  return wgrad_ws_bytes(geo.cs, geo.kh * geo.kw * geo.cb, (long)geo.n * geo.hs * geo.ws, split_k);
+}
+
 extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, const cv_operand* gout,
-                                       float* gweight, float* gbias, int split_k, cv_stream_t stream) {
+                                       float* gweight, float* gbias, int split_k, float* work, size_t work_bytes,
+                                       cv_stream_t stream) {
   clear_error();
   if (check_conv(g) || check_operand(in, "conv_backward_weight") || check_operand(gout, "conv_backward_weight"))
     return 1;
@@ -897,8 +990,8 @@ extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, c
   const Geo geo = geo_of(g);
   CV_REQUIRE(!g->transposed || !gbias, "convT bias gradient is not a WGRAD column (use a reduction)");
   // conv: small = dY, big = X ; convT: small = X, big = dY
-  if (!g->transposed) return run_wgrad(geo, gout, in, gweight, gbias, split_k, S(stream));
-  return run_wgrad(geo, in, gout, gweight, nullptr, split_k, S(stream));
+  if (!g->transposed) return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream));
+  return run_wgrad(geo, in, gout, gweight, nullptr, split_k, work, work_bytes, S(stream));
 }
 
 // ---------------------------------------------------------------- linear layers
@@ -982,8 +1075,14 @@ extern "C" int cv_linear_backward_data(const cv_linear* g, const cv_operand* gou
   return linear_launch(a, accumulate, S(stream));
 }
 
+extern "C" size_t cv_linear_wgrad_workspace_bytes(const cv_linear* g, int split_k) {
+  if (!g) return 0;
+  return wgrad_ws_bytes(g->out_features, g->in_features, g->n, split_k);
+}
+
 extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
-                                         float* gweight, float* gbias, int split_k, cv_stream_t stream) {
+                                         float* gweight, float* gbias, int split_k, float* work, size_t work_bytes,
+                                         cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(g && g->n > 0, "linear_backward_weight: bad geometry");
   if (check_operand(gout, "linear_backward_weight") || check_operand(in, "linear_backward_weight")) return 1;
@@ -1005,5 +1104,5 @@ extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* g
   }
   geo.s = 1;
   geo.p = 0;
-  return run_wgrad(geo, gout, in, gweight, gbias, split_k, S(stream));
+  return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream));
 }

@@ -19,7 +19,9 @@ import torch  # noqa: F401  (must be imported before the HIP library is dlopen'e
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libclearvae_hip.so")
 
-STAT_REPL = 8
+def stat_repl(C: int) -> int:
+    """CV_STAT_REPL(C) of include/clearvae.h: replicas of a C-feature fp64 statistics buffer."""
+    return 8 if C >= 256 else 16 if C >= 128 else 32 if C >= 64 else 64 if C >= 32 else 128 if C >= 16 else 256
 
 XF_NONE, XF_BNRELU, XF_BNBWD = 0, 1, 2
 STAT_NONE, STAT_FWD, STAT_BWD = 0, 1, 2
@@ -127,8 +129,10 @@ _SIGS = {
     "cv_conv_backward_data": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_weight": (
         c_int,
-        [_P(cv_conv), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p],
+        [_P(cv_conv), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p],
     ),
+    "cv_conv_wgrad_workspace_bytes": (c_size_t, [_P(cv_conv), c_int]),
+    "cv_linear_wgrad_workspace_bytes": (c_size_t, [_P(cv_linear), c_int]),
     "cv_linear_forward": (
         c_int,
         [_P(cv_linear), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_int, _P(cv_epilogue), c_void_p],
@@ -139,7 +143,7 @@ _SIGS = {
     ),
     "cv_linear_backward_weight": (
         c_int,
-        [_P(cv_linear), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p],
+        [_P(cv_linear), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p],
     ),
     "cv_declinear_backward_weight": (
         c_int,

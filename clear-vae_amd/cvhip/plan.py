@@ -25,7 +25,6 @@ from ._lib import (
     STAT_BWD,
     STAT_FWD,
     STAT_NONE,
-    STAT_REPL,
     XF_BNBWD,
     XF_BNRELU,
     XF_NONE,
@@ -393,14 +392,15 @@ class Workspace:
         # fp64 statistics arena: per BN layer [REPL,2,C] forward + [REPL,2,C] backward, plus scalars
         bns = spec.bn_layers
         counts = [n * c.h_out * c.w_out for c in spec.enc] + [n] + [n * c.h_out * c.w_out for c in spec.dec]
-        tot = sum(2 * STAT_REPL * 2 * b.num_features for b in bns) + 16
+        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 16
         self.stats = torch.zeros(tot, dtype=torch.float64, device=device)
         self.bnv = []
         o = 0
         for b, cnt in zip(bns, counts):
-            sz = STAT_REPL * 2 * b.num_features
-            st = self.stats[o:o + sz].view(STAT_REPL, 2, b.num_features)
-            gs = self.stats[o + sz:o + 2 * sz].view(STAT_REPL, 2, b.num_features)
+            R = _lib.stat_repl(b.num_features)
+            sz = R * 2 * b.num_features
+            st = self.stats[o:o + sz].view(R, 2, b.num_features)
+            gs = self.stats[o + sz:o + 2 * sz].view(R, 2, b.num_features)
             self.bnv.append(BNView(b, st, gs, cnt))
             o += 2 * sz
         self.scal = self.stats[o:o + 16]  # [0] rec sum, [1] mse work
@@ -416,6 +416,14 @@ class Workspace:
             self.lse = torch.empty(2, 2 * n, **f32)  # contrastive row log-sum-exps (2 branches)
             self.losses = torch.zeros(8, **f32)
             self.mi_work = torch.zeros(int(_lib.lib().cv_mi_workspace_bytes(n)) // 4 + 16, **f32)
+            # split-K partial tiles of the weight-gradient GEMMs (one launch at a time on the stream)
+            L = _lib.lib()
+            C, Hh, Wh = spec.feat
+            wb = [int(L.cv_conv_wgrad_workspace_bytes(ctypes.byref(c.geom(n)), 0)) for c in spec.enc + spec.dec]
+            wb.append(int(L.cv_linear_wgrad_workspace_bytes(
+                ctypes.byref(cv_linear(n, spec.F, 4 * d, Hh * Wh, C, 1, 0)), 0)))
+            self.wg_bytes = max(wb + [16])
+            self.wg_work = torch.empty(self.wg_bytes // 4, **f32)
 
     # -- programs --------------------------------------------------------------------------
     def forward_program(self, x: torch.Tensor, train: bool, eps=None, seed: int = 0, offset=None,
@@ -500,7 +508,8 @@ class Workspace:
             else:
                 P.add("cv_conv_backward_data", g, gout, c.wbwd, self.gah, ep_none())
                 xin = operand(self.ah)
-            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0)
+            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
+                  self.wg_bytes)
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
         P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
@@ -516,7 +525,7 @@ class Workspace:
         lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
         a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
         P.add("cv_linear_backward_weight", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
-              param_grad(sp.heads[0].bias), 0)
+              param_grad(sp.heads[0].bias), 0, self.wg_work, self.wg_bytes)
         ep = ep_bwd(self.bn_enc[-1], self.y_enc[-1], True, stat_div=Hh * Wh)
         P.add("cv_linear_backward_data", lin, operand(dheads), sp.heads[0].weight, self.g_enc[-1], 0, ep)
         for li in range(len(sp.enc) - 1, -1, -1):
@@ -531,7 +540,8 @@ class Workspace:
                 if dx is not None:
                     P.add("cv_conv_backward_data", g, gout, c.wbwd, dx, ep_none())
                 xin = operand(x, nchw=1)
-            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0)
+            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
+                  self.wg_bytes)
 
     def bn_grads_program(self, P: Program, param_grad, which: str = "all"):
         views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]

@@ -12,7 +12,7 @@
  *   - activations are NHWC fp32 ("pixels x channels" row-major); weights keep PyTorch's layouts
  *     (Conv2d [Cout][Cin][kh][kw], ConvTranspose2d [Cin][Cout][kh][kw], Linear [out][in]);
  *   - BatchNorm batch statistics are accumulated in fp64 by the producing kernel's epilogue into
- *     CV_STAT_REPL replicas of [2][C] doubles (sum, sum of squares / sum dz, sum dz*xhat) and folded
+ *     CV_STAT_REPL(C) replicas of [2][C] doubles (sum, sum of squares / sum dz, sum dz*xhat) and folded
  *     into per-channel constants by the consuming kernel's prologue (the normalised activation is
  *     never written to HBM);
  *   - return value 0 = success; otherwise cv_last_error() describes the failure (host-side checks
@@ -30,14 +30,16 @@ extern "C" {
 
 typedef void* cv_stream_t; /* a hipStream_t (torch.cuda.current_stream().cuda_stream) */
 
-#define CV_STAT_REPL 8
+/* Replicas of a C-feature statistics buffer: narrow layers get more replicas so that the fp64
+ * atomics of thousands of producer workgroups do not serialise on a few addresses. */
+#define CV_STAT_REPL(C) ((C) >= 256 ? 8 : (C) >= 128 ? 16 : (C) >= 64 ? 32 : (C) >= 32 ? 64 : (C) >= 16 ? 128 : 256)
 
 /* ---- BatchNorm as seen by a fused prologue/epilogue (nn.BatchNorm1d/2d, vae.py:17-44, 115-154) ---- */
 typedef struct cv_bn {
   const float* gamma;        /* [C] PyTorch order                                              */
   const float* beta;         /* [C]                                                            */
-  const double* stat;        /* [REPL][2][C] forward sums (sum x, sum x^2) of the layer input  */
-  const double* gstat;       /* [REPL][2][C] backward sums (sum dz, sum dz*xhat)               */
+  const double* stat;        /* [CV_STAT_REPL(C)][2][C] forward sums (sum x, sum x^2)         */
+  const double* gstat;       /* [CV_STAT_REPL(C)][2][C] backward sums (sum dz, sum dz*xhat)   */
   const float* running_mean; /* [C]                                                            */
   const float* running_var;  /* [C]                                                            */
   int C;                     /* normalised features                                            */
@@ -107,10 +109,14 @@ int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float*
                           float* gin, const cv_epilogue* ep, cv_stream_t stream);
 
 /* dw += sum_pixels T(x) (x) T(dy).  Replaces the grad_weight half of aten::convolution_backward.
- * split_k <= 0 picks a split; gweight (and gbias) must be zeroed by the caller (atomic
- * accumulation).  gbias (optional, Conv2d only) += sum_pixels T(dy). */
+ * gbias (optional, Conv2d only) += sum_pixels T(dy).  The pixel sum is split over workgroups
+ * (split_k <= 0: automatic); the partial tiles go to `work` (cv_conv_wgrad_workspace_bytes) and one
+ * reduction launch adds them into gweight/gbias.  With work == NULL the partials are fp32 atomics
+ * into gweight/gbias instead (correct, slower).  Either way the result is added to gweight/gbias. */
+size_t cv_conv_wgrad_workspace_bytes(const cv_conv* g, int split_k);
 int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, const cv_operand* gout,
-                            float* gweight, float* gbias, int split_k, cv_stream_t stream);
+                            float* gweight, float* gbias, int split_k, float* work, size_t work_bytes,
+                            cv_stream_t stream);
 
 /* ---- fully connected layers (nn.Linear heads vae.py:27-30; decoder Linear vae.py:33) ----
  * A linear layer whose input (or output) is the NCHW-flattened view of an NHWC activation with
@@ -127,8 +133,11 @@ int cv_linear_forward(const cv_linear* g, const cv_operand* in, const float* wei
                       cv_stream_t stream);
 int cv_linear_backward_data(const cv_linear* g, const cv_operand* gout, const float* weight,
                             float* gin, int accumulate, const cv_epilogue* ep, cv_stream_t stream);
+/* dW += sum_n gout[n] (x) T(in[n]) (+ gbias), same split/workspace contract as the conv version. */
+size_t cv_linear_wgrad_workspace_bytes(const cv_linear* g, int split_k);
 int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
-                              float* gweight, float* gbias, int split_k, cv_stream_t stream);
+                              float* gweight, float* gbias, int split_k, float* work, size_t work_bytes,
+                              cv_stream_t stream);
 
 /* Decoder Linear -> BatchNorm1d -> ReLU backward (vae.py:33-35).  da: gradient w.r.t. the ReLU
  * output in the Unflatten/NHWC order (g->out_pix, g->out_ch); h: the Linear output (BN1d input),

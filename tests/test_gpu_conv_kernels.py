@@ -10,7 +10,6 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-REPL = 8
 TOL = 1e-5
 
 
@@ -41,7 +40,9 @@ def _bn_state(C, count, rng, dev):
 def _stats_of(t_nhwc, C):
     """fp64 replica-0 sums of an NHWC tensor (sum, sum of squares)."""
     v = t_nhwc.double().reshape(-1, C)
-    st = torch.zeros(REPL, 2, C, dtype=torch.float64, device=t_nhwc.device)
+    from cvhip import _lib
+
+    st = torch.zeros(_lib.stat_repl(C), 2, C, dtype=torch.float64, device=t_nhwc.device)
     st[0, 0] = v.sum(0)
     st[0, 1] = (v * v).sum(0)
     return st
@@ -120,7 +121,7 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
     out = torch.empty(n, hout, hout, cout, dtype=torch.float32, device=dev)
     ep = _lib.cv_epilogue()
     ep.stat_mode, ep.stat_div = _lib.STAT_FWD, 1
-    st_out = torch.zeros(REPL, 2, cout, dtype=torch.float64, device=dev)
+    st_out = torch.zeros(_lib.stat_repl(cout), 2, cout, dtype=torch.float64, device=dev)
     ep.stat_out = st_out.data_ptr()
     _lib.call("cv_conv_forward", g, opnd, Wf.data_ptr(), b.data_ptr(), out.data_ptr(), ep, s_)
     xin_nchw = xin_host.permute(0, 3, 1, 2).cpu()
@@ -140,7 +141,7 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
         go_, bo_ = _bn_state(cout, n * hout * hout, rng, dev)
         st_o = _stats_of(yo, cout)
         dz = dyo
-        gst = torch.zeros(REPL, 2, cout, dtype=torch.float64, device=dev)
+        gst = torch.zeros(_lib.stat_repl(cout), 2, cout, dtype=torch.float64, device=dev)
         v = yo.double().reshape(-1, cout)
         xh = (v - v.mean(0)) / torch.sqrt(v.var(0, unbiased=False) + 1e-5)
         gst[0, 0] = dz.double().reshape(-1, cout).sum(0)
@@ -161,15 +162,28 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
     gref = gref.permute(0, 2, 3, 1)
     torch.cuda.synchronize()
     assert rel(gin, gref) < TOL, ("backward_data", rel(gin, gref))
-    # ---------------- weight gradient
+    # ---------------- weight gradient (+ bias column when the layout allows): split-K partial tiles
+    # through the workspace, then again with fp32 atomics (work = NULL)
+    with_bias = (not tr) and (k * k * cin) % 4 == 0
+    wb = _lib.lib().cv_conv_wgrad_workspace_bytes(g, 0)
+    work = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
     gw = torch.zeros(wshape, dtype=torch.float32, device=dev)
-    _lib.call("cv_conv_backward_weight", g, opnd, gop, gw.data_ptr(), None, 0, s_)
+    gb = torch.zeros(cout, dtype=torch.float32, device=dev)
+    _lib.call("cv_conv_backward_weight", g, opnd, gop, gw.data_ptr(), gb.data_ptr() if with_bias else None, 0,
+              work.data_ptr(), wb, s_)
+    gw_at = torch.full(wshape, 0.5, dtype=torch.float32, device=dev)  # accumulates onto existing values
+    _lib.call("cv_conv_backward_weight", g, opnd, gop, gw_at.data_ptr(), None, 0, None, 0, s_)
     if tr:
         wref = torch.nn.grad.conv2d_weight(dy_nchw, (cin, cout, k, k), xin_nchw, stride=s, padding=p)
     else:
         wref = torch.nn.grad.conv2d_weight(xin_nchw, wshape, dy_nchw, stride=s, padding=p)
     torch.cuda.synchronize()
     assert rel(gw, wref) < TOL, ("backward_weight", rel(gw, wref))
+    assert rel(gw_at - 0.5, wref) < TOL, ("backward_weight atomics", rel(gw_at - 0.5, wref))
+    if with_bias:  # (a BN-backward dy sums to ~0 per channel: compare against the sum of |dy|)
+        bref = dy_nchw.sum((0, 2, 3))
+        err = float((gb.double().cpu() - bref).abs().max())
+        assert err <= TOL * float(dy_nchw.abs().sum((0, 2, 3)).max()), ("bias grad", err)
 
 
 @pytest.mark.parametrize("geom", [g for g in GEOMS if g[2] not in (1, 3)],
@@ -191,7 +205,7 @@ def test_backward_data_stat_epilogue(geom):
     gi, bi = _bn_state(cin, n * hin * hin, rng, dev)
     rm, rv = torch.zeros(cin, device=dev), torch.ones(cin, device=dev)
     st_i = _stats_of(yin, cin)
-    gst = torch.zeros(REPL, 2, cin, dtype=torch.float64, device=dev)
+    gst = torch.zeros(_lib.stat_repl(cin), 2, cin, dtype=torch.float64, device=dev)
     ep = _lib.cv_epilogue()
     ep.stat_mode, ep.stat_div = _lib.STAT_BWD, 1
     ep.stat_out = gst.data_ptr()
