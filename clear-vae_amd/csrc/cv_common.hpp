@@ -35,6 +35,19 @@ void clear_error();
 static inline hipStream_t S(cv_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// generic conv geometry: small grid S (hs x ws x cs), big grid B (hb x wb x cb), yb = ys*s - p + kh.
+// Conv2d: small = output, big = input; ConvTranspose2d: small = input, big = output.
+struct Geo {
+  int n, hs, ws, cs, hb, wb, cb, kh, kw, s, p;
+};
+
+// direct (VALU) kernels for convs with <= 4 channels on one side (cv_narrow.hip); return -1 when
+// the geometry is not one they serve, else 0 / error code
+int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const float* bias, float* out,
+                  const cv_epilogue* ep, hipStream_t st);
+int narrow_scatter(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
+                   const cv_epilogue* ep, hipStream_t st);
+
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -31,10 +31,6 @@ constexpr int NT = 256;
 
 enum { OP_GATHER = 0, OP_SCATTER = 1, OP_WGRAD = 2, OP_DENSE = 3 };
 
-// generic geometry shared by the conv problems (small grid S, big grid B, yb = ys*s - p + kh)
-struct Geo {
-  int n, hs, ws, cs, hb, wb, cb, kh, kw, s, p;
-};
 
 struct Args {
   int op;
@@ -638,29 +634,44 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
 }
 
 // ------------------------------------------------------------------ split-K reduction of WGRAD
-// gw[row][c][tap] += sum_s part[s][row][tap*cb + c]; gbias[row] += sum_s part[s][row][N]
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int split, int M, int N,
-                                                           int ntot, int cb, int kk, float* gw, float* gbias) {
-  const long total = (long)M * N + (gbias ? M : 0);
+// gw[row][c][tap] += sum_s part[s][row][tap*cb + c]; gbias[row] += sum_s part[s][row][N].
+// Block = 64 consecutive partial-tile elements x 4 split groups; blockIdx.y takes a slice of the
+// splits (fp32 atomics combine the slices when gridDim.y > 1), so every thread sums <= ~8 slabs.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int split, int zper,
+                                                           int M, int N, int ntot, int cb, int kk, float* gw,
+                                                           float* gbias) {
+  __shared__ float red[4][64];
+  const int t = threadIdx.x, ol = t & 63, zg = t >> 6;
+  const long o = (long)blockIdx.x * 64 + ol;  // element of the [M][ntot] partial tile
+  const long total = (long)M * ntot;
   const size_t sstride = (size_t)M * ntot;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    int row, col;
+  const int z0 = blockIdx.y * zper, z1 = min(split, z0 + zper);
+  float acc = 0.f;
+  if (o < total) {
+    const float* p = part + o;
+    int z = z0 + zg;
+    for (; z + 12 < z1; z += 16) {
+      const float a0 = p[(size_t)z * sstride], a1 = p[(size_t)(z + 4) * sstride];
+      const float a2 = p[(size_t)(z + 8) * sstride], a3 = p[(size_t)(z + 12) * sstride];
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; z < z1; z += 4) acc += p[(size_t)z * sstride];
+  }
+  red[zg][ol] = acc;
+  __syncthreads();
+  if (t < 64 && o < total) {
+    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    const int row = (int)(o / ntot), col = (int)(o - (long)row * ntot);
     float* dst;
-    if (i < (long)M * N) {
-      row = (int)(i / N);
-      const int rem = (int)(i - (long)row * N);
-      const int c = rem / kk, tap = rem - c * kk;
-      col = tap * cb + c;
-      dst = gw + i;
+    if (col < N) {
+      const int tap = col / cb, c = col - tap * cb;
+      dst = gw + ((size_t)row * cb + c) * kk + tap;
     } else {
-      row = (int)(i - (long)M * N);
-      col = N;
+      if (!gbias) return;
       dst = gbias + row;
     }
-    const float* p = part + (size_t)row * ntot + col;
-    float acc = 0.f;
-    for (int z = 0; z < split; ++z) acc += p[z * sstride];
-    *dst += acc;
+    if (gridDim.y == 1) *dst += v;
+    else atomicAdd(dst, v);
   }
 }
 
@@ -806,6 +817,8 @@ static int check_conv(const cv_conv* g) {
 // GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
 static int run_gather(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                       const cv_epilogue* ep, hipStream_t st, const char* what) {
+  const int nr = narrow_gather(g, in, w, bias, out, ep, st);
+  if (nr >= 0) return nr;
   Args a;
   init_args(a);
   a.op = OP_GATHER;
@@ -829,6 +842,8 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
 // SCATTER with big = rows. `in` is the small-grid tensor; w is packed [tap][cs][cb].
 static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                        const cv_epilogue* ep, hipStream_t st, const char* what) {
+  const int nr = narrow_scatter(g, in, w, bias, out, ep, st);
+  if (nr >= 0) return nr;
   Args a;
   init_args(a);
   a.op = OP_SCATTER;
@@ -913,11 +928,12 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   }
   if (launch(a, w.BM, w.BN, w.split, st)) return 1;
   if (a.part) {
-    const long total = (long)a.M * a.N + (gbias ? a.M : 0);
-    long blocks = (total + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, work, w.split, a.M, a.N, Ntot, g.cb,
-                       g.kh * g.kw, gw, gbias);
+    const int gx = cdiv((long)a.M * Ntot, 64);
+    int gy = cdiv(w.split, 32);  // <= 32 slabs per block (8 per thread)
+    const int zper = cdiv(w.split, gy);
+    gy = cdiv(w.split, zper);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, work, w.split, zper, a.M, a.N, Ntot,
+                       g.cb, g.kh * g.kw, gw, gbias);
     CV_LAUNCH_CHECK("wgrad_reduce");
   }
   return 0;
