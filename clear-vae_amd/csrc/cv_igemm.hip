@@ -65,10 +65,8 @@ __device__ __forceinline__ float xf_apply(const cv_operand& o, const XfA& c, int
   return x;
 }
 
-__device__ __forceinline__ float4 xf_apply4(const cv_operand& o, const XfA& c, int ch0, float4 v, const float* yp) {
+__device__ __forceinline__ float4 xf_apply4(const cv_operand& o, const XfA& c, int ch0, float4 v, float4 yy) {
   if (o.xf == CV_XF_NONE) return v;
-  float4 yy = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (o.xf == CV_XF_BNBWD) yy = *reinterpret_cast<const float4*>(yp);
   v.x = xf_apply(o, c, ch0 + 0, v.x, yy.x);
   v.y = xf_apply(o, c, ch0 + 1, v.y, yy.y);
   v.z = xf_apply(o, c, ch0 + 2, v.z, yy.z);
@@ -103,24 +101,36 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ float4 z4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // ------------------------------------------------------------------ the kernel
-template <int BM, int BN>
+// Operand staging: global -> registers (raw values, a validity mask) -> [after the MFMAs of the
+// current tile] BatchNorm transform -> LDS.  Deferring the transform to the store keeps the next
+// tile's loads in flight across the current tile's MFMAs (a transform at load time would wait for
+// them immediately).
+//
+// LDS images:
+//   row-oriented A (GATHER/SCATTER/DENSE): [BK/4 quads][BM rows][4 k] -- the ds_write_b128 of a
+//     (row, quad) staging float4 is contiguous, and the 64 lanes of an MFMA A-fragment read
+//     (16 rows x 4 k) are 64 consecutive floats (bank-conflict free);
+//   WGRAD A: [BK][BM + 16] k-major (staged as float4 along M);
+//   B: [BK][BN (+16)] k-major.
+template <int OP, int BM, int BN>
 __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   constexpr int WN = (BN >= 32) ? 2 : 1;
   constexpr int WM = 4 / WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(FM >= 1 && FN >= 1, "tile too small");
-  constexpr int LDA = BM + 16;                              // (BM+16) % 32 == 16: conflict-free reads
+  constexpr bool ROWS = OP != OP_WGRAD;
+  constexpr int LDA = ROWS ? BM : BM + 16;
   constexpr int LDB = BN + ((BN % 32) == 0 ? 16 : 0);
   constexpr int RA = BM / 32;                               // A rows per thread (row-oriented)
   constexpr int AW = (BM * BK / 4 + NT - 1) / NT;           // WGRAD A float4 per thread
   constexpr int BW = (BN * BK / 4 + NT - 1) / NT;           // B float4 per thread
-  constexpr int RAW = RA > AW ? RA : AW;
-  constexpr int ABUF = BK * LDA, BBUF = BK * LDB;
+  constexpr int RAW = ROWS ? RA : AW;
+  constexpr int ABUF = BK * LDA + (ROWS ? 0 : 0), BBUF = BK * LDB;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;                     // [2][BK][LDA]
-  float* Bs = As + 2 * ABUF;            // [2][BK][LDB]
+  float* As = smem;                     // [2][ABUF]
+  float* Bs = As + 2 * ABUF;            // [2][BBUF]
   float* red = Bs + 2 * BBUF;           // epilogue reduction scratch: 2 * WM * BN floats
   float* cstA = red + 2 * WM * BN;      // BN constants
   float* cstB = cstA + xf_floats(P.a.xf, P.ca_n);
@@ -128,26 +138,26 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int op = P.op;
+  const Geo& g = P.g;
 
   // ---------------- block -> (m0, n0, k-range, class)
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   int M = P.M, K = P.K;
-  const int N = P.N + ((op == OP_WGRAD && P.gbias) ? 1 : 0);
+  const int N = P.N + ((OP == OP_WGRAD && P.gbias) ? 1 : 0);
   int kbeg = 0, kend = K;
   int ry = 0, rx = 0, yb0 = 0, xb0 = 0, cy = 1, cx = 1, ntx = 1;
-  if (op == OP_SCATTER) {
-    const int s = P.g.s, cls = blockIdx.z;
+  if (OP == OP_SCATTER) {
+    const int s = g.s, cls = blockIdx.z;
     ry = cls / s;
     rx = cls % s;
-    yb0 = (((ry - P.g.p) % s) + s) % s;  // big rows with (yb + p) % s == ry
-    xb0 = (((rx - P.g.p) % s) + s) % s;
-    cy = (P.g.hb > yb0) ? (P.g.hb - yb0 + s - 1) / s : 0;
-    cx = (P.g.wb > xb0) ? (P.g.wb - xb0 + s - 1) / s : 0;
-    const int nty = (P.g.kh > ry) ? (P.g.kh - ry + s - 1) / s : 0;
-    ntx = (P.g.kw > rx) ? (P.g.kw - rx + s - 1) / s : 0;
-    M = P.g.n * cy * cx;
-    K = nty * ntx * P.g.cs;
+    yb0 = (((ry - g.p) % s) + s) % s;  // big rows with (yb + p) % s == ry
+    xb0 = (((rx - g.p) % s) + s) % s;
+    cy = (g.hb > yb0) ? (g.hb - yb0 + s - 1) / s : 0;
+    cx = (g.wb > xb0) ? (g.wb - xb0 + s - 1) / s : 0;
+    const int nty = (g.kh > ry) ? (g.kh - ry + s - 1) / s : 0;
+    ntx = (g.kw > rx) ? (g.kw - rx + s - 1) / s : 0;
+    M = g.n * cy * cx;
+    K = nty * ntx * g.cs;
     kend = K;
     if (m0 >= M) return;
   } else {
@@ -156,10 +166,9 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     if (kbeg >= kend) return;
   }
 
-  // ---------------- prologue: BN constants into LDS
-  // (the A tile buffers are not live yet: they serve as the fold's scratch)
+  // ---------------- prologue: BN constants into LDS (the A buffers serve as the fold's scratch)
   double* fold_scratch = reinterpret_cast<double*>(As);
-  static_assert(2 * BK * LDA * sizeof(float) >= 4 * NT * sizeof(double), "fold scratch");
+  static_assert(2 * BK * (ROWS ? BM : BM + 16) * sizeof(float) >= 4 * NT * sizeof(double), "fold scratch");
   XfA ca, cb;
   fill_consts(P.a, P.ca_n, cstA, fold_scratch, ca);
   fill_consts(P.b, P.cb_n, cstB, fold_scratch, cb);
@@ -170,31 +179,30 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     });
   }
 
-  // ---------------- per-thread A-row decode (row-oriented problems): rows (t&15)+16*(t>>7)+32*i,
-  // K quad (t>>4)&7 of the 32-deep tile
+  // ---------------- per-thread A-row decode (row-oriented): rows (t&15)+16*(t>>7)+32*i, quad (t>>4)&7
   const int quad = (t >> 4) & 7;
   int r_n[RA], r_y[RA], r_x[RA];
   bool r_ok[RA];
-  if (op != OP_WGRAD) {
+  if (ROWS) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int r = m0 + (t & 15) + 16 * (t >> 7) + 32 * i;
       r_ok[i] = r < M;
       const int rr = r_ok[i] ? r : 0;
-      if (op == OP_GATHER) {
-        const int hw = P.g.hs * P.g.ws;
+      if (OP == OP_GATHER) {
+        const int hw = g.hs * g.ws;
         r_n[i] = rr / hw;
         const int rem = rr - r_n[i] * hw;
-        const int ys = rem / P.g.ws, xs = rem - ys * P.g.ws;
-        r_y[i] = ys * P.g.s - P.g.p;  // big-grid origin of the receptive field
-        r_x[i] = xs * P.g.s - P.g.p;
-      } else if (op == OP_SCATTER) {
+        const int ys = rem / g.ws, xs = rem - ys * g.ws;
+        r_y[i] = ys * g.s - g.p;  // big-grid origin of the receptive field
+        r_x[i] = xs * g.s - g.p;
+      } else if (OP == OP_SCATTER) {
         const int hw = cy * cx;
         r_n[i] = rr / hw;
         const int rem = rr - r_n[i] * hw;
         const int ty = rem / cx, tx = rem - ty * cx;
-        r_y[i] = yb0 + P.g.s * ty + P.g.p;  // (yb + p); ys = (r_y - kh) / s
-        r_x[i] = xb0 + P.g.s * tx + P.g.p;
+        r_y[i] = yb0 + g.s * ty + g.p;  // (yb + p); ys = (r_y - kh) / s
+        r_x[i] = xb0 + g.s * tx + g.p;
       } else {
         r_n[i] = rr;
         r_y[i] = 0;
@@ -204,29 +212,80 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   }
   __syncthreads();
 
-  float4 ra[RAW];
-  float4 rb[BW];
+  // launch-uniform choice between the vectorised (deferred-transform) and scalar operand paths
+  const bool a_vec = (OP == OP_GATHER) ? ((g.cb & 3) == 0 && !P.a.nchw)
+                   : (OP == OP_SCATTER) ? ((g.cs & 3) == 0)
+                   : (OP == OP_DENSE) ? ((P.lda & 3) == 0 && (P.K & 3) == 0 && (P.a_pix == 1 || (P.a_ch & 3) == 0))
+                   : ((g.cs & 3) == 0);
+  const bool b_vec = (OP == OP_WGRAD) && (g.cb & 3) == 0 && !P.b.nchw;
+  const bool a_bwd = P.a.xf == CV_XF_BNBWD, b_bwd = P.b.xf == CV_XF_BNBWD;
 
-  // ---------------- operand fetchers
+  float4 ra[RAW], rya[RAW];
+  float4 rb[BW], ryb[BW];
+  unsigned amask = 0, bmask = 0;
+
+  // DENSE: the K loop runs in the storage order of A (k' = pix*a_ch + c for an NCHW-flattened
+  // input); lf() is the PyTorch feature index of k' (weight column / BN1d feature)
+  auto lf = [&](int kk) -> int {
+    if (P.a_pix <= 1) return kk;
+    const int pix = kk / P.a_ch, c = kk - pix * P.a_ch;
+    return c * P.a_pix + pix;
+  };
+
+  // ---------------- A: fetch raw values into registers
   auto fetchA = [&](int k0) {
-    const Geo& g = P.g;
-    if (op == OP_GATHER) {
+    amask = 0;
+    if (ROWS) {
       const int kq = k0 + 4 * quad;
-      if ((g.cb & 3) == 0 && !P.a.nchw) {
-        // the 4 k of this quad share one tap: one division per tile
-        const int tap = kq / g.cb, c0 = kq - tap * g.cb;
-        const int kh = tap / g.kw, kw = tap - kh * g.kw;
+      if (a_vec) {
+        if (OP == OP_GATHER) {
+          const int tap = kq / g.cb, c0 = kq - tap * g.cb;
+          const int kh = tap / g.kw, kw = tap - kh * g.kw;
 #pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          float4 v = z4();
-          const int yb = r_y[i] + kh, xb = r_x[i] + kw;
-          if (r_ok[i] && kq < kend && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
-            const size_t off = ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
-            v = xf_apply4(P.a, ca, c0, ld4(P.a.x + off), P.a.y + off);
+          for (int i = 0; i < RA; ++i) {
+            const int yb = r_y[i] + kh, xb = r_x[i] + kw;
+            ra[i] = z4();
+            rya[i] = z4();
+            if (r_ok[i] && kq < kend && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
+              const size_t off = ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
+              ra[i] = ld4(P.a.x + off);
+              if (a_bwd) rya[i] = ld4(P.a.y + off);
+              amask |= 1u << i;
+            }
           }
-          ra[i] = v;
+        } else if (OP == OP_SCATTER) {
+          const int tap = kq / g.cs, c0 = kq - tap * g.cs;
+          const int jy = tap / ntx, jx = tap - jy * ntx;
+          const int kh = ry + g.s * jy, kw = rx + g.s * jx;
+#pragma unroll
+          for (int i = 0; i < RA; ++i) {
+            const int py = r_y[i] - kh, px = r_x[i] - kw;  // divisible by s by construction
+            ra[i] = z4();
+            rya[i] = z4();
+            if (r_ok[i] && kq < kend && py >= 0 && px >= 0) {
+              const int ys = py / g.s, xs = px / g.s;
+              if (ys < g.hs && xs < g.ws) {
+                const size_t off = ((size_t)(r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c0;
+                ra[i] = ld4(P.a.x + off);
+                if (a_bwd) rya[i] = ld4(P.a.y + off);
+                amask |= 1u << i;
+              }
+            }
+          }
+        } else {  // DENSE, storage-order k'
+#pragma unroll
+          for (int i = 0; i < RA; ++i) {
+            ra[i] = z4();
+            rya[i] = z4();
+            if (r_ok[i] && kq < kend) {
+              const size_t off = (size_t)r_n[i] * P.lda + kq;
+              ra[i] = ld4(P.a.x + off);
+              if (a_bwd) rya[i] = ld4(P.a.y + off);
+              amask |= 1u << i;
+            }
+          }
         }
-      } else {  // first conv (C = 1 or 3, NCHW input) / last convT backward (C = 1 or 3)
+      } else {  // scalar path (transform applied here)
 #pragma unroll
         for (int i = 0; i < RA; ++i) {
           float tmp[4];
@@ -234,151 +293,128 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           for (int j = 0; j < 4; ++j) {
             tmp[j] = 0.f;
             const int k = kq + j;
-            if (r_ok[i] && k < kend) {
+            if (!r_ok[i] || k >= kend) continue;
+            size_t off;
+            int ch;
+            bool ok = true;
+            if (OP == OP_GATHER) {
               const int tap = k / g.cb, c = k - tap * g.cb;
               const int kh = tap / g.kw, kw = tap - kh * g.kw;
               const int yb = r_y[i] + kh, xb = r_x[i] + kw;
-              if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
-                const size_t off = P.a.nchw ? ((size_t)(r_n[i] * g.cb + c) * g.hb + yb) * g.wb + xb
-                                            : ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c;
-                const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
-                tmp[j] = xf_apply(P.a, ca, c, P.a.x[off], yv);
-              }
-            }
-          }
-          ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
-        }
-      }
-    } else if (op == OP_SCATTER) {
-      const int kq = k0 + 4 * quad;
-      if ((g.cs & 3) == 0) {
-        const int tap = kq / g.cs, c0 = kq - tap * g.cs;
-        const int jy = tap / ntx, jx = tap - jy * ntx;
-        const int kh = ry + g.s * jy, kw = rx + g.s * jx;
-#pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          float4 v = z4();
-          const int py = r_y[i] - kh, px = r_x[i] - kw;  // divisible by s by construction
-          if (r_ok[i] && kq < kend && py >= 0 && px >= 0) {
-            const int ys = py / g.s, xs = px / g.s;
-            if (ys < g.hs && xs < g.ws) {
-              const size_t off = ((size_t)(r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c0;
-              v = xf_apply4(P.a, ca, c0, ld4(P.a.x + off), P.a.y + off);
-            }
-          }
-          ra[i] = v;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          float tmp[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            tmp[j] = 0.f;
-            const int k = kq + j;
-            if (r_ok[i] && k < kend) {
+              ok = (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
+              off = P.a.nchw ? ((size_t)(r_n[i] * g.cb + c) * g.hb + yb) * g.wb + xb
+                             : ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c;
+              ch = c;
+            } else if (OP == OP_SCATTER) {
               const int tap = k / g.cs, c = k - tap * g.cs;
               const int jy = tap / ntx, jx = tap - jy * ntx;
               const int py = r_y[i] - (ry + g.s * jy), px = r_x[i] - (rx + g.s * jx);
-              if (py >= 0 && px >= 0 && py / g.s < g.hs && px / g.s < g.ws) {
-                const size_t off = ((size_t)(r_n[i] * g.hs + py / g.s) * g.ws + px / g.s) * g.cs + c;
-                const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
-                tmp[j] = xf_apply(P.a, ca, c, P.a.x[off], yv);
-              }
+              ok = py >= 0 && px >= 0 && py / g.s < g.hs && px / g.s < g.ws;
+              off = ((size_t)(r_n[i] * g.hs + (ok ? py / g.s : 0)) * g.ws + (ok ? px / g.s : 0)) * g.cs + c;
+              ch = c;
+            } else {
+              off = (size_t)r_n[i] * P.lda + k;
+              const int f = lf(k);
+              ch = (P.ca_n == P.K) ? f : (P.a_pix > 1 ? k % P.a_ch : f);
+            }
+            if (ok) {
+              const float yv = a_bwd ? P.a.y[off] : 0.f;
+              tmp[j] = xf_apply(P.a, ca, ch, P.a.x[off], yv);
             }
           }
           ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         }
       }
-    } else if (op == OP_DENSE) {
-      const int kq = k0 + 4 * quad;
-#pragma unroll
-      for (int i = 0; i < RA; ++i) {
-        float tmp[4];
-        if (P.a_pix == 1 && (P.lda & 3) == 0 && kq + 3 < kend && r_ok[i]) {
-          const size_t off = (size_t)r_n[i] * P.lda + kq;
-          const float4 v = xf_apply4(P.a, ca, kq, ld4(P.a.x + off), P.a.y + off);
-          tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int k = kq + j;
-            tmp[j] = 0.f;
-            if (r_ok[i] && k < kend) {
-              const int col = (P.a_pix > 1) ? (k % P.a_pix) * P.a_ch + k / P.a_pix : k;
-              const size_t off = (size_t)r_n[i] * P.lda + col;
-              const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off] : 0.f;
-              // constants are per logical feature k (BN1d) or per channel k / a_pix (BN2d)
-              tmp[j] = xf_apply(P.a, ca, (P.ca_n == K) ? k : k / P.a_pix, P.a.x[off], yv);
-            }
-          }
-        }
-        ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
-      }
-    } else {  // OP_WGRAD: A(m = cs, k = small pixel) = T(small[pix][cs]); float4 along cs
+    } else {  // WGRAD A(m = cs, k = small pixel): float4 along cs
       constexpr int MQ = BM / 4;
 #pragma unroll
       for (int e = 0; e < AW; ++e) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
         const int pix = k0 + kk, c0 = m0 + 4 * mq;
-        float4 v = z4();
+        ra[e] = z4();
+        rya[e] = z4();
         if (kk < BK && pix < kend) {
           const size_t off = (size_t)pix * g.cs + c0;
-          if ((g.cs & 3) == 0) {
-            if (c0 < g.cs) v = xf_apply4(P.a, ca, c0, ld4(P.a.x + off), P.a.y + off);
+          if (a_vec) {
+            if (c0 < g.cs) {
+              ra[e] = ld4(P.a.x + off);
+              if (a_bwd) rya[e] = ld4(P.a.y + off);
+              amask |= 1u << e;
+            }
           } else {
             float tmp[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               tmp[j] = 0.f;
               if (c0 + j < g.cs) {
-                const float yv = (P.a.xf == CV_XF_BNBWD) ? P.a.y[off + j] : 0.f;
+                const float yv = a_bwd ? P.a.y[off + j] : 0.f;
                 tmp[j] = xf_apply(P.a, ca, c0 + j, P.a.x[off + j], yv);
               }
             }
-            v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+            ra[e] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
         }
-        ra[e] = v;
       }
     }
   };
 
-  auto storeA = [&](float* Ab) {
-    if (op == OP_WGRAD) {
+  // ---------------- A: transform (vector paths) + store to LDS
+  auto storeA = [&](float* Ab, int k0) {
+    if (ROWS) {
+      const int kq = k0 + 4 * quad;
+      int ch0 = 0;
+      if (a_vec && P.a.xf != CV_XF_NONE) {
+        if (OP == OP_GATHER) ch0 = kq % g.cb;
+        else if (OP == OP_SCATTER) ch0 = kq % g.cs;
+        else ch0 = (P.a_pix > 1) ? kq % P.a_ch : kq;
+      }
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        float4 v = ra[i];
+        if (a_vec && P.a.xf != CV_XF_NONE) {
+          if (amask & (1u << i)) {
+            if (OP == OP_DENSE && P.a_pix > 1 && P.ca_n == P.K) {  // BN1d over NCHW-order features
+              const int pix = kq / P.a_ch;
+              float vv[4] = {v.x, v.y, v.z, v.w};
+              const float yy[4] = {rya[i].x, rya[i].y, rya[i].z, rya[i].w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) vv[e] = xf_apply(P.a, ca, (ch0 + e) * P.a_pix + pix, vv[e], yy[e]);
+              v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            } else {
+              v = xf_apply4(P.a, ca, ch0, v, rya[i]);
+            }
+          }
+        }
+        const int m = (t & 15) + 16 * (t >> 7) + 32 * i;
+        *reinterpret_cast<float4*>(Ab + (quad * BM + m) * 4) = v;
+      }
+    } else {
       constexpr int MQ = BM / 4;
 #pragma unroll
       for (int e = 0; e < AW; ++e) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
-        if (kk < BK) *reinterpret_cast<float4*>(Ab + kk * LDA + 4 * mq) = ra[e];
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < RA; ++i) {
-        const int m = (t & 15) + 16 * (t >> 7) + 32 * i;
-        float* p = Ab + (4 * quad) * LDA + m;
-        p[0] = ra[i].x;
-        p[LDA] = ra[i].y;
-        p[2 * LDA] = ra[i].z;
-        p[3 * LDA] = ra[i].w;
+        float4 v = ra[e];
+        if (a_vec && P.a.xf != CV_XF_NONE && (amask & (1u << e))) v = xf_apply4(P.a, ca, m0 + 4 * mq, v, rya[e]);
+        if (kk < BK) *reinterpret_cast<float4*>(Ab + kk * LDA + 4 * mq) = v;
       }
     }
   };
 
-  // B: one float4 of a K row (4 consecutive columns) per slot; rows kk, column quad nq
+  // ---------------- B: one float4 of a K row (4 consecutive columns) per slot
   constexpr int NQ = BN / 4;
   auto fetchB = [&](int k0) {
-    const Geo& g = P.g;
+    bmask = 0;
 #pragma unroll
     for (int e = 0; e < BW; ++e) {
       const int idx = t + NT * e;
       const int nq = idx % NQ, kk = idx / NQ;
       const int col = n0 + 4 * nq, k = k0 + kk;
       float4 v = z4();
+      ryb[e] = z4();
       if (kk < BK && k < kend && col < N) {
-        if (op == OP_GATHER) {  // packed [K = tap*cb][cs]
+        if (OP == OP_GATHER) {  // packed [K = tap*cb][cs]
           if (col + 3 < N && (g.cs & 3) == 0) {
             v = ld4(P.w + (size_t)k * g.cs + col);
           } else {
@@ -386,7 +422,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
             for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)k * g.cs + col + j];
             v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
-        } else if (op == OP_SCATTER) {  // packed [tap][cs][cb]; class taps
+        } else if (OP == OP_SCATTER) {  // packed [tap][cs][cb]; class taps
           const int tap = k / g.cs, c = k - tap * g.cs;
           const int jy = tap / ntx, jx = tap - jy * ntx;
           const int kh = ry + g.s * jy, kw = rx + g.s * jx;
@@ -398,17 +434,18 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
             for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[rowo + col + j];
             v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
-        } else if (op == OP_DENSE) {
+        } else if (OP == OP_DENSE) {
+          const int kl = lf(k);
           float tmp[4] = {0.f, 0.f, 0.f, 0.f};
           if (P.wlayout) {
             if (col + 3 < N && (P.ldb & 3) == 0) {
-              v = ld4(P.w + (size_t)k * P.ldb + col);
+              v = ld4(P.w + (size_t)kl * P.ldb + col);
               tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
             } else {
-              for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)k * P.ldb + col + j];
+              for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)kl * P.ldb + col + j];
             }
           } else {
-            for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)(col + j) * P.ldb + k];
+            for (int j = 0; j < 4 && col + j < N; ++j) tmp[j] = P.w[(size_t)(col + j) * P.ldb + kl];
           }
           v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         } else {  // WGRAD: B(k = small pixel, col = (tap, cb)) = T(big[gather(pix, tap)][cb])
@@ -418,13 +455,15 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           const int nreal = P.N;
           if (col >= nreal) {  // bias column (nreal % 4 == 0 when gbias is used)
             v = make_float4(col == nreal ? 1.f : 0.f, 0.f, 0.f, 0.f);
-          } else if ((g.cb & 3) == 0 && !P.b.nchw) {
+          } else if (b_vec) {
             const int tap = col / g.cb, c0 = col - tap * g.cb;
             const int kh = tap / g.kw, kw = tap - kh * g.kw;
             const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
             if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
               const size_t off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + c0;
-              v = xf_apply4(P.b, cb, c0, ld4(P.b.x + off), P.b.y + off);
+              v = ld4(P.b.x + off);
+              if (b_bwd) ryb[e] = ld4(P.b.y + off);
+              bmask |= 1u << e;
             }
           } else {
             float tmp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -436,7 +475,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
               if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
                 const size_t off = P.b.nchw ? ((size_t)(nimg * g.cb + c) * g.hb + yb) * g.wb + xb
                                             : ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + c;
-                const float yv = (P.b.xf == CV_XF_BNBWD) ? P.b.y[off] : 0.f;
+                const float yv = b_bwd ? P.b.y[off] : 0.f;
                 tmp[j] = xf_apply(P.b, cb, c, P.b.x[off], yv);
               }
             }
@@ -457,7 +496,12 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     for (int e = 0; e < BW; ++e) {
       const int idx = t + NT * e;
       const int nq = idx % NQ, kk = idx / NQ;
-      if (kk < BK) *reinterpret_cast<float4*>(Bb + kk * LDB + 4 * nq) = rb[e];
+      float4 v = rb[e];
+      if (OP == OP_WGRAD && b_vec && P.b.xf != CV_XF_NONE && (bmask & (1u << e))) {
+        const int col = n0 + 4 * nq;
+        v = xf_apply4(P.b, cb, col % g.cb, v, ryb[e]);
+      }
+      if (kk < BK) *reinterpret_cast<float4*>(Bb + kk * LDB + 4 * nq) = v;
     }
   };
 
@@ -470,7 +514,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
 
   fetchA(kbeg);
   fetchB(kbeg);
-  storeA(As);
+  storeA(As, kbeg);
   storeB(Bs);
   __syncthreads();
   int cur = 0;
@@ -487,7 +531,10 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
       const int kr = kk + (lane >> 4);
       float av[FM], bv[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) av[i] = Ab[kr * LDA + wm * TM + i * 16 + (lane & 15)];
+      for (int i = 0; i < FM; ++i) {
+        const int m = wm * TM + i * 16 + (lane & 15);
+        av[i] = ROWS ? Ab[((kk >> 2) * BM + m) * 4 + (lane >> 4)] : Ab[kr * LDA + m];
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j) bv[j] = Bb[kr * LDB + wn * TN + j * 16 + (lane & 15)];
 #pragma unroll
@@ -497,7 +544,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      storeA(As + (cur ^ 1) * ABUF);
+      storeA(As + (cur ^ 1) * ABUF, k0 + BK);
       storeB(Bs + (cur ^ 1) * BBUF);
     }
     __syncthreads();
@@ -520,12 +567,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
         const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
         float v = acc[i][j][r];
         if (row >= M || col >= N) continue;
-        if (op == OP_WGRAD) {
+        if (OP == OP_WGRAD) {
           if (P.part) {  // plain store of this split's partial tile; wgrad_reduce_kernel sums them
             P.part[((size_t)blockIdx.z * M + row) * N + col] = v;
             continue;
           }
-          const Geo& g = P.g;
           const int tap = col / g.cb, c = col - tap * g.cb;  // w layout [cs][cb][kh][kw]
           float* dst = (col >= P.N) ? P.gbias + row : P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap;
           if (gridDim.z == 1) *dst += v;  // single writer
@@ -533,14 +579,14 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           continue;
         }
         size_t off;
-        if (op == OP_GATHER) {
-          off = (size_t)row * P.g.cs + col;
-        } else if (op == OP_SCATTER) {
+        if (OP == OP_GATHER) {
+          off = (size_t)row * g.cs + col;
+        } else if (OP == OP_SCATTER) {
           const int hw = cy * cx;
           const int nimg = row / hw, rem = row - nimg * hw;
           const int ty = rem / cx, tx = rem - ty * cx;
-          const int yb = yb0 + P.g.s * ty, xb = xb0 + P.g.s * tx;
-          off = ((size_t)(nimg * P.g.hb + yb) * P.g.wb + xb) * P.g.cb + col;
+          const int yb = yb0 + g.s * ty, xb = xb0 + g.s * tx;
+          off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + col;
         } else {
           const int oc = (P.o_pix > 1) ? (col % P.o_pix) * P.o_ch + col / P.o_pix : col;
           off = (size_t)row * P.ldo + oc;
@@ -569,7 +615,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     }
   }
 
-  if (stats && !P.accumulate && op != OP_WGRAD) {
+  if (OP != OP_WGRAD && stats && !P.accumulate) {
     // reduce per column: lanes with equal (lane & 15), then the WM waves sharing wn
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -678,28 +724,40 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // ------------------------------------------------------------------ host-side launch
 static size_t lds_bytes(const Args& a, int BM_, int BN_) {
   const int WN = (BN_ >= 32) ? 2 : 1, WM = 4 / WN;
-  const int LDA = BM_ + 16, LDB = BN_ + ((BN_ % 32) == 0 ? 16 : 0);
+  const int LDA = (a.op == OP_WGRAD) ? BM_ + 16 : BM_, LDB = BN_ + ((BN_ % 32) == 0 ? 16 : 0);
   size_t f = 2 * ((size_t)BK * LDA + (size_t)BK * LDB) + 2 * WM * BN_;
   f += xf_floats(a.a.xf, a.ca_n) + xf_floats(a.b.xf, a.cb_n);
   if (a.ep.stat_mode == CV_STAT_BWD) f += 4 * (size_t)a.ce_n;
   return f * sizeof(float);
 }
 
-template <int BM, int BN>
+template <int OP, int BM, int BN>
 static int launch_t(const Args& a, dim3 grid, hipStream_t st) {
   const size_t lds = lds_bytes(a, BM, BN);
   CV_REQUIRE(lds <= 160 * 1024, "igemm: LDS request %zu bytes exceeds 160 KiB", lds);
   if (lds > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)igemm_kernel<BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)igemm_kernel<OP, BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL((igemm_kernel<BM, BN>), grid, dim3(NT), lds, st, a);
+  hipLaunchKernelGGL((igemm_kernel<OP, BM, BN>), grid, dim3(NT), lds, st, a);
   CV_LAUNCH_CHECK("igemm");
   return 0;
+}
+
+template <int OP>
+static int launch_op(const Args& a, int BM_, int BN_, dim3 grid, hipStream_t st) {
+  if (BM_ == 128 && BN_ == 64) return launch_t<OP, 128, 64>(a, grid, st);
+  if (BM_ == 128 && BN_ == 32) return launch_t<OP, 128, 32>(a, grid, st);
+  if (BM_ == 128 && BN_ == 16) return launch_t<OP, 128, 16>(a, grid, st);
+  if (BM_ == 64 && BN_ == 64) return launch_t<OP, 64, 64>(a, grid, st);
+  if (BM_ == 64 && BN_ == 32) return launch_t<OP, 64, 32>(a, grid, st);
+  if (BM_ == 64 && BN_ == 16) return launch_t<OP, 64, 16>(a, grid, st);
+  cv::set_error("igemm: unsupported tile %dx%d", BM_, BN_);
+  return 1;
 }
 
 static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
@@ -708,14 +766,12 @@ static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
   dim3 grid(gx, gy, gz);
   CV_REQUIRE(gx > 0 && gy > 0 && gz > 0, "igemm: empty grid");
   CV_REQUIRE(gx < (1 << 30) && gy < 65536 && gz < 65536, "igemm: grid too large");
-  if (BM_ == 128 && BN_ == 64) return launch_t<128, 64>(a, grid, st);
-  if (BM_ == 128 && BN_ == 32) return launch_t<128, 32>(a, grid, st);
-  if (BM_ == 128 && BN_ == 16) return launch_t<128, 16>(a, grid, st);
-  if (BM_ == 64 && BN_ == 64) return launch_t<64, 64>(a, grid, st);
-  if (BM_ == 64 && BN_ == 32) return launch_t<64, 32>(a, grid, st);
-  if (BM_ == 64 && BN_ == 16) return launch_t<64, 16>(a, grid, st);
-  cv::set_error("igemm: unsupported tile %dx%d", BM_, BN_);
-  return 1;
+  switch (a.op) {
+    case OP_GATHER: return launch_op<OP_GATHER>(a, BM_, BN_, grid, st);
+    case OP_SCATTER: return launch_op<OP_SCATTER>(a, BM_, BN_, grid, st);
+    case OP_WGRAD: return launch_op<OP_WGRAD>(a, BM_, BN_, grid, st);
+    default: return launch_op<OP_DENSE>(a, BM_, BN_, grid, st);
+  }
 }
 
 // Row-oriented tile: prefer 64-wide N tiles, shrink N (keeping BM=64) until there are >= 512
