@@ -73,31 +73,39 @@ def conv_flops_per_image(spec):
     return 3 * f
 
 
-def kernel_pass(engine, G, steps=3):
-    """Run the step program eagerly with a HIP event pair around every C-ABI call (on the stream the
-    kernels are launched on) and return {call label: mean ms}."""
+def kernel_pass(engine, G, reps=20, rounds=3):
+    """Per-call device time of the step program: each C-ABI call is captured REPS times back to back
+    into its own HIP graph (torch.cuda.CUDAGraph on the stream the kernels are launched on) and the
+    graph replay is bracketed by HIP events, so the average excludes host launch gaps.  Returns
+    {call label: mean ms per launch}.  (Repeating a call perturbs the workspace; run after timing.)"""
     from cvhip import _lib
 
     progs = [("fwd", G["fwd"]), ("dec", G["dec"]), ("lat", G["lat"]), ("enc", G["enc"]), ("upd", G["upd"])]
     if G.get("learn") is not None:
         progs.append(("learn", G["learn"]))
-    s = _lib.stream_handle()
     times = {}
-    for _ in range(steps):
-        evs = []
-        for pname, P in progs:
-            for i, (name, fn, args) in enumerate(P.calls):
+    for pname, P in progs:
+        for i, (name, fn, args) in enumerate(P.calls):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                s = _lib.stream_handle()
+                for _ in range(reps):
+                    _lib.check(fn(*args, s), name)
+            g.replay()
+            torch.cuda.synchronize()
+            best = None
+            for _ in range(rounds):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-                rc = fn(*args, s)
+                g.replay()
                 e1.record()
-                _lib.check(rc, name)
-                evs.append((f"{pname}[{i}]:{name}", e0, e1, args))
-        torch.cuda.synchronize()
-        for label, e0, e1, _ in evs:
-            times.setdefault(label, []).append(e0.elapsed_time(e1))
-    return {k: sum(v) / len(v) for k, v in times.items()}
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                best = ms if best is None else min(best, ms)
+            times[f"{pname}[{i}]:{name}"] = best
+            del g
+    return times
 
 
 def gemm_flops_of(label, G, engine):
@@ -258,7 +266,7 @@ def main():
     roof = None
     if not args.no_kernel_pass:
         G = eng.graphs[B]
-        km = kernel_pass(eng, G, steps=5)
+        km = kernel_pass(eng, G)
         best = None
         for label, ms in km.items():
             fl = gemm_flops_of(label, G, eng)

@@ -124,15 +124,28 @@ __device__ __forceinline__ BnBwdC bn_bwd_const_s(const cv_bn& b, int c, double s
   return r;
 }
 
-// serial replica fold of one feature (a single thread; fine for wide layers, R <= 16)
-__device__ __forceinline__ void bn_sums(const double* st, int C, int c, double& s, double& q) {
+// replica fold of one feature: replicas r0, r0+G, ... < R of [R][2][C] (loads issued 4 at a time)
+__device__ __forceinline__ void bn_sums_g(const double* st, int C, int c, int r0, int G, int R, double& s, double& q) {
   s = 0.0;
   q = 0.0;
   if (!st) return;
-  for (int r = 0, R = CV_STAT_REPL(C); r < R; ++r) {
+  int r = r0;
+  for (; r + 3 * G < R; r += 4 * G) {
+    const double* p0 = st + (size_t)r * 2 * C + c;
+    const size_t d = (size_t)G * 2 * C;
+    const double a0 = p0[0], a1 = p0[d], a2 = p0[2 * d], a3 = p0[3 * d];
+    const double b0 = p0[C], b1 = p0[d + C], b2 = p0[2 * d + C], b3 = p0[3 * d + C];
+    s += (a0 + a1) + (a2 + a3);
+    q += (b0 + b1) + (b2 + b3);
+  }
+  for (; r < R; r += G) {
     s += st[(size_t)r * 2 * C + c];
     q += st[(size_t)r * 2 * C + C + c];
   }
+}
+
+__device__ __forceinline__ void bn_sums(const double* st, int C, int c, double& s, double& q) {
+  bn_sums_g(st, C, c, 0, 1, CV_STAT_REPL(C), s, q);
 }
 
 __device__ __forceinline__ void bn_mean_istd(const cv_bn& b, int c, float& mean, float& istd) {
@@ -180,14 +193,8 @@ __device__ __forceinline__ void bn_fold(const cv_bn& b, bool with_g, double* scr
     const int f = t / G, j = t - f * G;
     double s = 0.0, q = 0.0, gs = 0.0, gq = 0.0;
     if (f < C) {
-      for (int r = j; r < R; r += G) {
-        s += b.stat[(size_t)r * 2 * C + f];
-        q += b.stat[(size_t)r * 2 * C + C + f];
-        if (with_g) {
-          gs += b.gstat[(size_t)r * 2 * C + f];
-          gq += b.gstat[(size_t)r * 2 * C + C + f];
-        }
-      }
+      bn_sums_g(b.stat, C, f, j, G, R, s, q);
+      if (with_g) bn_sums_g(b.gstat, C, f, j, G, R, gs, gq);
     }
     scratch[t] = s;
     scratch[NT + t] = q;

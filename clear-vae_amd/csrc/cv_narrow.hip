@@ -56,11 +56,17 @@ __device__ __forceinline__ void stats_flush(const float* s1, const float* s2, do
 }
 
 // ---------------------------------------------------------------- narrow gather (cs = 32 outputs)
-template <int CS>
+// thread = (output pixel, channel quad): 8 lanes share a pixel (same input loads, coalesced by the
+// memory pipeline) and each owns a float4 of output channels, so a wave stores 1 KiB contiguously.
+// The KK x KK x CB receptive field is loaded in one unrolled burst before any arithmetic, so a
+// thread waits for one memory latency per pixel, not one per tap.
+template <int CS, int KK, int CB>
 __global__ __launch_bounds__(NNT) void narrow_gather_kernel(const NArgs P) {
-  constexpr int KMAX = 64;
-  __shared__ float4 Ws[KMAX * CS / 4];
-  __shared__ float bs[CS];
+  constexpr int K = KK * KK * CB;
+  constexpr int NQ = CS / 4;          // lanes per pixel
+  constexpr int PPB = NNT / NQ;       // pixels per block iteration
+  __shared__ float4 Ws[K * NQ];
+  __shared__ float4 bs[NQ];
   __shared__ BnFwdC kf[4];
   __shared__ BnBwdC kb[4];
   __shared__ BnFwdC ke[CS];
@@ -68,14 +74,16 @@ __global__ __launch_bounds__(NNT) void narrow_gather_kernel(const NArgs P) {
   __shared__ float red[(NNT / 64) * 2 * CS];
   const int t = threadIdx.x;
   const Geo& g = P.g;
-  const int K = g.kh * g.kw * g.cb;
-  for (int i = t; i < K * CS / 4; i += NNT) Ws[i] = reinterpret_cast<const float4*>(P.w)[i];
-  for (int i = t; i < CS; i += NNT) bs[i] = P.bias ? P.bias[i] : 0.f;
-  if (P.a.xf == CV_XF_BNRELU)
+  for (int i = t; i < K * NQ; i += NNT) Ws[i] = reinterpret_cast<const float4*>(P.w)[i];
+  for (int i = t; i < NQ; i += NNT)
+    bs[i] = P.bias ? make_float4(P.bias[4 * i], P.bias[4 * i + 1], P.bias[4 * i + 2], P.bias[4 * i + 3])
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int xf = P.a.xf;
+  if (xf == CV_XF_BNRELU)
     bn_fold<NNT>(P.a.bn, false, scratch, [&](int f, double s, double q, double, double) {
       if (f < 4) kf[f] = bn_fwd_const_s(P.a.bn, f, s, q);
     });
-  else if (P.a.xf == CV_XF_BNBWD)
+  else if (xf == CV_XF_BNBWD)
     bn_fold<NNT>(P.a.bn, true, scratch, [&](int f, double s, double q, double gs, double gq) {
       if (f < 4) kb[f] = bn_bwd_const_s(P.a.bn, f, s, q, gs, gq);
     });
@@ -86,95 +94,122 @@ __global__ __launch_bounds__(NNT) void narrow_gather_kernel(const NArgs P) {
     });
   __syncthreads();
 
-  float s1[CS], s2[CS];
-#pragma unroll
-  for (int j = 0; j < CS; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  const int q = t % NQ, pl = t / NQ;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   const int hw = g.hs * g.ws;
-  for (long p = (long)blockIdx.x * NNT + t; p < P.M; p += (long)gridDim.x * NNT) {
+  for (long p = (long)blockIdx.x * PPB + pl; p < P.M; p += (long)gridDim.x * PPB) {
     const int n = (int)(p / hw);
     const int rem = (int)(p - (long)n * hw);
     const int ys = rem / g.ws, xs = rem - ys * g.ws;
     const int y0 = ys * g.s - g.p, x0 = xs * g.s - g.p;
-    float acc[CS];
+    float v[K], yv[K];
+    unsigned long long okm = 0;  // receptive-field validity (zero padding stays 0 after the transform)
 #pragma unroll
-    for (int j = 0; j < CS; ++j) acc[j] = bs[j];
-    for (int kh = 0; kh < g.kh; ++kh) {
-      const int yb = y0 + kh;
-      if ((unsigned)yb >= (unsigned)g.hb) continue;
-      for (int kw = 0; kw < g.kw; ++kw) {
-        const int xb = x0 + kw;
-        if ((unsigned)xb >= (unsigned)g.wb) continue;
-        for (int c = 0; c < g.cb; ++c) {
-          const size_t off = P.a.nchw ? ((size_t)(n * g.cb + c) * g.hb + yb) * g.wb + xb
-                                      : ((size_t)(n * g.hb + yb) * g.wb + xb) * g.cb + c;
-          float v = P.a.x[off];
-          if (P.a.xf == CV_XF_BNRELU) v = bn_relu(v, kf[c]);
-          else if (P.a.xf == CV_XF_BNBWD) v = bn_bwd(v, P.a.y[off], kb[c]);
-          const float4* wr = Ws + ((kh * g.kw + kw) * g.cb + c) * (CS / 4);
+    for (int kh = 0; kh < KK; ++kh)
 #pragma unroll
-          for (int j = 0; j < CS / 4; ++j) {
-            const float4 w4 = wr[j];
-            acc[4 * j + 0] = fmaf(v, w4.x, acc[4 * j + 0]);
-            acc[4 * j + 1] = fmaf(v, w4.y, acc[4 * j + 1]);
-            acc[4 * j + 2] = fmaf(v, w4.z, acc[4 * j + 2]);
-            acc[4 * j + 3] = fmaf(v, w4.w, acc[4 * j + 3]);
+      for (int kw = 0; kw < KK; ++kw)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+          const int i = (kh * KK + kw) * CB + c;
+          const int yb = y0 + kh, xb = x0 + kw;
+          v[i] = 0.f;
+          yv[i] = 0.f;
+          if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
+            const size_t off = P.a.nchw ? ((size_t)(n * CB + c) * g.hb + yb) * g.wb + xb
+                                        : ((size_t)(n * g.hb + yb) * g.wb + xb) * CB + c;
+            v[i] = P.a.x[off];
+            if (xf == CV_XF_BNBWD) yv[i] = P.a.y[off];
+            okm |= 1ull << i;
           }
         }
-      }
+    float4 acc = bs[q];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int c = i % CB;
+      float a = v[i];
+      const bool ok = (okm >> i) & 1ull;
+      if (xf == CV_XF_BNRELU) a = ok ? bn_relu(a, kf[c]) : 0.f;
+      else if (xf == CV_XF_BNBWD) a = ok ? bn_bwd(a, yv[i], kb[c]) : 0.f;
+      const float4 w4 = Ws[i * NQ + q];
+      acc.x = fmaf(a, w4.x, acc.x);
+      acc.y = fmaf(a, w4.y, acc.y);
+      acc.z = fmaf(a, w4.z, acc.z);
+      acc.w = fmaf(a, w4.w, acc.w);
     }
-    float4* o4 = reinterpret_cast<float4*>(P.out + (size_t)p * CS);
+    float vv[4] = {acc.x, acc.y, acc.z, acc.w};
+    const size_t o = (size_t)p * CS + 4 * q;
     if (mode == CV_STAT_BWD) {
-      const float4* y4 = reinterpret_cast<const float4*>(P.ep.ey + (size_t)p * CS);
+      const float4 ey = *reinterpret_cast<const float4*>(P.ep.ey + o);
+      const float yy[4] = {ey.x, ey.y, ey.z, ey.w};
 #pragma unroll
-      for (int j = 0; j < CS / 4; ++j) {
-        const float4 yv = y4[j];
-        const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int ch = 4 * j + e;
-          float v = acc[ch];
-          if (P.ep.erelu && bn_out(yy[e], ke[ch]) <= 0.f) v = 0.f;
-          acc[ch] = v;
-          s1[ch] += v;
-          s2[ch] += v * ((yy[e] - ke[ch].mu) * ke[ch].istd);
-        }
+      for (int e = 0; e < 4; ++e) {
+        const BnFwdC k = ke[4 * q + e];
+        if (P.ep.erelu && bn_out(yy[e], k) <= 0.f) vv[e] = 0.f;
+        s1[e] += vv[e];
+        s2[e] += vv[e] * ((yy[e] - k.mu) * k.istd);
       }
     } else if (mode == CV_STAT_FWD) {
 #pragma unroll
-      for (int j = 0; j < CS; ++j) {
-        s1[j] += acc[j];
-        s2[j] += acc[j] * acc[j];
+      for (int e = 0; e < 4; ++e) {
+        s1[e] += vv[e];
+        s2[e] += vv[e] * vv[e];
       }
     }
-#pragma unroll
-    for (int j = 0; j < CS / 4; ++j) o4[j] = make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
+    *reinterpret_cast<float4*>(P.out + o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
   }
-  if (mode != CV_STAT_NONE) stats_flush<CS>(s1, s2, P.ep.stat_out, CS, red);
+  if (mode != CV_STAT_NONE) {
+    // lanes l, l^NQ, l^2NQ, ... own the same channel quad: butterfly over the pixel lanes
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = NQ; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    const int lane = t & 63, w = t >> 6;
+    if (lane < NQ) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[w * 2 * CS + 4 * lane + e] = s1[e];
+        red[w * 2 * CS + CS + 4 * lane + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    if (t < 2 * CS) {
+      double acc2 = 0.0;
+#pragma unroll
+      for (int w2 = 0; w2 < NNT / 64; ++w2) acc2 += (double)red[w2 * 2 * CS + t];
+      const int repl = blockIdx.x % CV_STAT_REPL(CS);
+      atomic_add_f64(P.ep.stat_out + (size_t)repl * 2 * CS + t, acc2);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- narrow scatter (cb <= 4 outputs)
-template <int CB>
+// 4 lanes per big-grid output pixel, each owning 8 of the CS = 32 input channels; the pixels of a
+// block belong to one stride-parity class (blockIdx.y), so every lane walks the same NT2 x NT2 taps.
+// All of a lane's tap loads are issued before any arithmetic; partial sums meet by two shuffles.
+template <int CB, int NT2>
 __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const Geo& g = P.g;
-  const int taps = g.kh * g.kw;
-  // LDS: Ws[tap][cs][CB] | BnFwdC/BnBwdC[cs] | scratch (4*NNT doubles) | red
-  float* Wl = sm;
-  float* kc = Wl + ((taps * g.cs * CB + 3) & ~3);
-  double* scratch = reinterpret_cast<double*>(kc + 8 * g.cs);
-  float* red = reinterpret_cast<float*>(scratch + 4 * NNT);
+  constexpr int CS = 32, LPP = 4, CPL = CS / LPP;  // channels per lane (2 float4)
+  constexpr int TP = NT2 * NT2;                      // taps of a class
+  __shared__ float Wl[16 * CS * CB];
+  __shared__ BnFwdC kf[CS];
+  __shared__ BnBwdC kb[CS];
+  __shared__ double scratch[4 * NNT];
+  __shared__ float red[(NNT / 64) * 2 * 4];
   __shared__ float bs[4];
   __shared__ BnFwdC ke[4];
+  const Geo& g = P.g;
   const int t = threadIdx.x;
-  for (int i = t; i < taps * g.cs * CB; i += NNT) Wl[i] = P.w[i];
+  for (int i = t; i < g.kh * g.kw * CS * CB; i += NNT) Wl[i] = P.w[i];
   if (t < CB) bs[t] = P.bias ? P.bias[t] : 0.f;
-  BnFwdC* kf = reinterpret_cast<BnFwdC*>(kc);
-  BnBwdC* kb = reinterpret_cast<BnBwdC*>(kc);
-  if (P.a.xf == CV_XF_BNRELU)
+  const int xf = P.a.xf;
+  if (xf == CV_XF_BNRELU)
     bn_fold<NNT>(P.a.bn, false, scratch, [&](int f, double s, double q, double, double) {
       kf[f] = bn_fwd_const_s(P.a.bn, f, s, q);
     });
-  else if (P.a.xf == CV_XF_BNBWD)
+  else if (xf == CV_XF_BNBWD)
     bn_fold<NNT>(P.a.bn, true, scratch, [&](int f, double s, double q, double gs, double gq) {
       kb[f] = bn_bwd_const_s(P.a.bn, f, s, q, gs, gq);
     });
@@ -185,69 +220,99 @@ __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
     });
   __syncthreads();
 
+  const int s = g.s, cls = blockIdx.y;
+  const int ry = cls / s, rx = cls % s;
+  const int yb0 = (((ry - g.p) % s) + s) % s, xb0 = (((rx - g.p) % s) + s) % s;
+  const int cy = (g.hb > yb0) ? (g.hb - yb0 + s - 1) / s : 0;
+  const int cx = (g.wb > xb0) ? (g.wb - xb0 + s - 1) / s : 0;
+  const int nty = (g.kh > ry) ? (g.kh - ry + s - 1) / s : 0;
+  const int ntx = (g.kw > rx) ? (g.kw - rx + s - 1) / s : 0;
+  const long Mc = (long)g.n * cy * cx;
+  const int sub = t % LPP, c0 = sub * CPL;
   float s1[CB], s2[CB];
 #pragma unroll
   for (int j = 0; j < CB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  const int hw = g.hb * g.wb;
-  const int cs4 = g.cs / 4;
-  for (long p = (long)blockIdx.x * NNT + t; p < P.M; p += (long)gridDim.x * NNT) {
-    const int n = (int)(p / hw);
-    const int rem = (int)(p - (long)n * hw);
-    const int yb = rem / g.wb, xb = rem - yb * g.wb;
-    float acc[CB];
+  const long rstride = (long)gridDim.x * (NNT / LPP);
+  // every lane runs the same trip count (the shuffles below need whole waves)
+  const long trips = (Mc + rstride - 1) / rstride;
+  for (long it = 0; it < trips; ++it) {
+    const long r = it * rstride + (long)blockIdx.x * (NNT / LPP) + t / LPP;
+    const bool live = r < Mc;
+    const long rr = live ? r : 0;
+    const int n = (int)(rr / (cy * cx));
+    const int rem = (int)(rr - (long)n * cy * cx);
+    const int ty = rem / cx, tx = rem - ty * cx;
+    const int yb = yb0 + s * ty, xb = xb0 + s * tx;
+    float4 xv[TP][2], yv4[TP][2];
+    bool ok[TP];
 #pragma unroll
-    for (int j = 0; j < CB; ++j) acc[j] = bs[j];
-    for (int kh = 0; kh < g.kh; ++kh) {
-      const int ty = yb + g.p - kh;
-      if (ty < 0) break;  // ty decreases with kh
-      const int ys = ty / g.s;
-      if (ys * g.s != ty || ys >= g.hs) continue;
-      for (int kw = 0; kw < g.kw; ++kw) {
-        const int tx = xb + g.p - kw;
-        if (tx < 0) break;
-        const int xs = tx / g.s;
-        if (xs * g.s != tx || xs >= g.ws) continue;
-        const size_t base = ((size_t)(n * g.hs + ys) * g.ws + xs) * g.cs;
-        const float* wt = Wl + (size_t)(kh * g.kw + kw) * g.cs * CB;
-        for (int c4 = 0; c4 < cs4; ++c4) {
-          float4 v = *reinterpret_cast<const float4*>(P.a.x + base + 4 * c4);
-          float vv[4] = {v.x, v.y, v.z, v.w};
-          if (P.a.xf == CV_XF_BNRELU) {
+    for (int jy = 0; jy < NT2; ++jy)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) vv[e] = bn_relu(vv[e], kf[4 * c4 + e]);
-          } else if (P.a.xf == CV_XF_BNBWD) {
-            const float4 y = *reinterpret_cast<const float4*>(P.a.y + base + 4 * c4);
-            const float yy[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) vv[e] = bn_bwd(vv[e], yy[e], kb[4 * c4 + e]);
+      for (int jx = 0; jx < NT2; ++jx) {
+        const int tp = jy * NT2 + jx;
+        const int kh = ry + s * jy, kw = rx + s * jx;
+        const int py = yb + g.p - kh, px = xb + g.p - kw;
+        const int ys = py / s, xs = px / s;
+        ok[tp] = live && jy < nty && jx < ntx && py >= 0 && px >= 0 && ys < g.hs && xs < g.ws;
+        xv[tp][0] = xv[tp][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        yv4[tp][0] = yv4[tp][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok[tp]) {
+          const float* src = P.a.x + ((size_t)(n * g.hs + ys) * g.ws + xs) * CS + c0;
+          xv[tp][0] = *reinterpret_cast<const float4*>(src);
+          xv[tp][1] = *reinterpret_cast<const float4*>(src + 4);
+          if (xf == CV_XF_BNBWD) {
+            const float* ysrc = P.a.y + ((size_t)(n * g.hs + ys) * g.ws + xs) * CS + c0;
+            yv4[tp][0] = *reinterpret_cast<const float4*>(ysrc);
+            yv4[tp][1] = *reinterpret_cast<const float4*>(ysrc + 4);
           }
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int j = 0; j < CB; ++j) acc[j] = fmaf(vv[e], wt[(4 * c4 + e) * CB + j], acc[j]);
         }
       }
+    float acc[CB];
+#pragma unroll
+    for (int j = 0; j < CB; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int jy = 0; jy < NT2; ++jy)
+#pragma unroll
+      for (int jx = 0; jx < NT2; ++jx) {
+        const int tp = jy * NT2 + jx;
+        if (!ok[tp]) continue;
+        const int kh = ry + s * jy, kw = rx + s * jx;
+        const float* wt = Wl + ((kh * g.kw + kw) * CS + c0) * CB;
+        const float xs8[8] = {xv[tp][0].x, xv[tp][0].y, xv[tp][0].z, xv[tp][0].w,
+                              xv[tp][1].x, xv[tp][1].y, xv[tp][1].z, xv[tp][1].w};
+        const float ys8[8] = {yv4[tp][0].x, yv4[tp][0].y, yv4[tp][0].z, yv4[tp][0].w,
+                              yv4[tp][1].x, yv4[tp][1].y, yv4[tp][1].z, yv4[tp][1].w};
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          float a = xs8[e];
+          if (xf == CV_XF_BNRELU) a = bn_relu(a, kf[c0 + e]);
+          else if (xf == CV_XF_BNBWD) a = bn_bwd(a, ys8[e], kb[c0 + e]);
+#pragma unroll
+          for (int j = 0; j < CB; ++j) acc[j] = fmaf(a, wt[e * CB + j], acc[j]);
+        }
+      }
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      acc[j] += __shfl_xor(acc[j], 1, 64);
+      acc[j] += __shfl_xor(acc[j], 2, 64);
     }
-    float* o = P.out + (size_t)p * CB;
-    if (mode == CV_STAT_BWD) {
+    if (live && sub == 0) {
+      const size_t po = ((size_t)(n * g.hb + yb) * g.wb + xb) * CB;
 #pragma unroll
       for (int j = 0; j < CB; ++j) {
-        const float yv = P.ep.ey[(size_t)p * CB + j];
-        float v = acc[j];
-        if (P.ep.erelu && bn_out(yv, ke[j]) <= 0.f) v = 0.f;
-        acc[j] = v;
-        s1[j] += v;
-        s2[j] += v * ((yv - ke[j].mu) * ke[j].istd);
-      }
-    } else if (mode == CV_STAT_FWD) {
-#pragma unroll
-      for (int j = 0; j < CB; ++j) {
-        s1[j] += acc[j];
-        s2[j] += acc[j] * acc[j];
+        float v = acc[j] + bs[j];
+        if (mode == CV_STAT_BWD) {
+          const float yv = P.ep.ey[po + j];
+          if (P.ep.erelu && bn_out(yv, ke[j]) <= 0.f) v = 0.f;
+          s1[j] += v;
+          s2[j] += v * ((yv - ke[j].mu) * ke[j].istd);
+        } else if (mode == CV_STAT_FWD) {
+          s1[j] += v;
+          s2[j] += v * v;
+        }
+        P.out[po + j] = v;
       }
     }
-#pragma unroll
-    for (int j = 0; j < CB; ++j) o[j] = acc[j];
   }
   if (mode != CV_STAT_NONE) stats_flush<CB>(s1, s2, P.ep.stat_out, CB, red);
 }
@@ -270,7 +335,7 @@ static int grid_for(long M) {
 
 int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const float* bias, float* out,
                   const cv_epilogue* ep, hipStream_t st) {
-  if (g.cb > 4 || g.cs != 32 || g.kh * g.kw * g.cb > 64) return -1;
+  if (g.cs != 32 || g.kh != g.kw || (g.kh != 3 && g.kh != 4) || (g.cb != 1 && g.cb != 3)) return -1;
   if (in->xf != CV_XF_NONE) CV_REQUIRE(in->bn.C == g.cb, "narrow_gather: BN width %d != %d", in->bn.C, g.cb);
   if (check_ep(ep, g.cs, "narrow_gather")) return 1;
   NArgs a;
@@ -283,14 +348,20 @@ int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const flo
   if (ep) a.ep = *ep;
   else a.ep.stat_mode = CV_STAT_NONE;
   a.M = (long)g.n * g.hs * g.ws;
-  hipLaunchKernelGGL(narrow_gather_kernel<32>, dim3(grid_for(a.M)), dim3(NNT), 0, st, a);
+  long blocks = (a.M + 31) / 32;  // 32 pixels per block iteration
+  if (blocks > 1024) blocks = 1024;
+  const dim3 grid((int)blocks), blk(NNT);
+  if (g.kh == 3 && g.cb == 1) hipLaunchKernelGGL((narrow_gather_kernel<32, 3, 1>), grid, blk, 0, st, a);
+  else if (g.kh == 3) hipLaunchKernelGGL((narrow_gather_kernel<32, 3, 3>), grid, blk, 0, st, a);
+  else if (g.cb == 1) hipLaunchKernelGGL((narrow_gather_kernel<32, 4, 1>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((narrow_gather_kernel<32, 4, 3>), grid, blk, 0, st, a);
   CV_LAUNCH_CHECK("narrow_gather");
   return 0;
 }
 
 int narrow_scatter(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
                    const cv_epilogue* ep, hipStream_t st) {
-  if (g.cb > 4 || (g.cs & 3) || g.cs > 256 || g.kh * g.kw > 16) return -1;
+  if (g.cb > 4 || g.cs != 32 || g.s != 2 || g.kh != g.kw || (g.kh != 3 && g.kh != 4)) return -1;
   if (in->xf != CV_XF_NONE) CV_REQUIRE(in->bn.C == g.cs, "narrow_scatter: BN width %d != %d", in->bn.C, g.cs);
   CV_REQUIRE(!in->nchw, "narrow_scatter: NHWC input required");
   if (check_ep(ep, g.cb, "narrow_scatter")) return 1;
@@ -304,15 +375,18 @@ int narrow_scatter(const Geo& g, const cv_operand* in, const float* ws, const fl
   if (ep) a.ep = *ep;
   else a.ep.stat_mode = CV_STAT_NONE;
   a.M = (long)g.n * g.hb * g.wb;
-  const size_t lds = (size_t)((g.kh * g.kw * g.cs * 4 + 3) & ~3) * 4 + 8 * g.cs * 4 + 4 * NNT * 8 + (NNT / 64) * 8 * 4;
-  CV_REQUIRE(lds <= 64 * 1024, "narrow_scatter: LDS %zu", lds);
-  const dim3 grid(grid_for(a.M)), blk(NNT);
+  const long rows = (long)g.n * cdiv(g.hb, g.s) * cdiv(g.wb, g.s);  // largest class
+  long bx = (rows + 63) / 64;  // 64 pixels per block iteration
+  if (bx > 512) bx = 512;       // bounds the fp64 atomics per statistics address
+  const dim3 grid((int)bx, g.s * g.s), blk(NNT);
+#define CV_NS(CBV) hipLaunchKernelGGL((narrow_scatter_kernel<CBV, 2>), grid, blk, 0, st, a)
   switch (g.cb) {
-    case 1: hipLaunchKernelGGL(narrow_scatter_kernel<1>, grid, blk, lds, st, a); break;
-    case 2: hipLaunchKernelGGL(narrow_scatter_kernel<2>, grid, blk, lds, st, a); break;
-    case 3: hipLaunchKernelGGL(narrow_scatter_kernel<3>, grid, blk, lds, st, a); break;
-    default: hipLaunchKernelGGL(narrow_scatter_kernel<4>, grid, blk, lds, st, a); break;
+    case 1: CV_NS(1); break;
+    case 2: CV_NS(2); break;
+    case 3: CV_NS(3); break;
+    default: CV_NS(4); break;
   }
+#undef CV_NS
   CV_LAUNCH_CHECK("narrow_scatter");
   return 0;
 }

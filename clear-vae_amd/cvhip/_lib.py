@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(_HERE, "libclearvae_hip.so")
 
 def stat_repl(C: int) -> int:
     """CV_STAT_REPL(C) of include/clearvae.h: replicas of a C-feature fp64 statistics buffer."""
-    return 8 if C >= 256 else 16 if C >= 128 else 32 if C >= 64 else 64 if C >= 32 else 128 if C >= 16 else 256
+    return 8 if C >= 256 else 16 if C >= 64 else 32
 
 XF_NONE, XF_BNRELU, XF_BNBWD = 0, 1, 2
 STAT_NONE, STAT_FWD, STAT_BWD = 0, 1, 2

@@ -162,19 +162,21 @@ class ParamArena:
     def __init__(self, params: list, device):
         self.params = list(params)
         self.device = torch.device(device)
-        total = sum(p.numel() for p in self.params)
-        self.numel = total
-        self.flat = torch.empty(total, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(total, dtype=torch.float32, device=self.device)
+        # every parameter starts on a 16-byte boundary (float4 loads); the gaps stay zero and get zero
+        # gradients, so Adam leaves them at zero
         self.offset = {}
         o = 0
+        for p in self.params:
+            self.offset[id(p)] = (o, p.numel())
+            o = (o + p.numel() + 3) & ~3
+        self.numel = o
+        self.flat = torch.zeros(o, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(o, dtype=torch.float32, device=self.device)
         with torch.no_grad():
             for p in self.params:
-                n = p.numel()
+                o, n = self.offset[id(p)]
                 self.flat[o:o + n].copy_(p.data.reshape(-1).to(self.device, torch.float32))
                 p.data = self.flat[o:o + n].view_as(p)
-                self.offset[id(p)] = (o, n)
-                o += n
 
     def valid(self) -> bool:
         base = self.flat.data_ptr()

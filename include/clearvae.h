@@ -32,7 +32,7 @@ typedef void* cv_stream_t; /* a hipStream_t (torch.cuda.current_stream().cuda_st
 
 /* Replicas of a C-feature statistics buffer: narrow layers get more replicas so that the fp64
  * atomics of thousands of producer workgroups do not serialise on a few addresses. */
-#define CV_STAT_REPL(C) ((C) >= 256 ? 8 : (C) >= 128 ? 16 : (C) >= 64 ? 32 : (C) >= 32 ? 64 : (C) >= 16 ? 128 : 256)
+#define CV_STAT_REPL(C) ((C) >= 256 ? 8 : (C) >= 64 ? 16 : 32)
 
 /* ---- BatchNorm as seen by a fused prologue/epilogue (nn.BatchNorm1d/2d, vae.py:17-44, 115-154) ---- */
 typedef struct cv_bn {
