@@ -208,6 +208,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-pass", action="store_true")
     ap.add_argument("--kernel-table", default=None, help="write the per-call timing table to this file")
+    ap.add_argument("--only-call", default=None,
+                    help="profiling mode: after warmup, launch this step-program call (e.g. 'enc[4]') --reps "
+                         "times back to back and exit (for rocprofv3 --pmc)")
+    ap.add_argument("--reps", type=int, default=50)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +248,18 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    if args.only_call:
+        from cvhip import _lib
+
+        G = eng.graphs[B]
+        pname, idx = args.only_call.split("[")
+        name, fn, cargs = G[pname].calls[int(idx.rstrip("]"))]
+        s_ = _lib.stream_handle()
+        for _ in range(args.reps):
+            _lib.check(fn(*cargs, s_), name)
+        torch.cuda.synchronize()
+        print(json.dumps({"only_call": args.only_call, "name": name, "reps": args.reps}))
+        return
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -280,6 +296,16 @@ def main():
             roof = {"bound": "mfma", "kernel": label, "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None,
                     "kernel_ms": round(ms, 5), "flops_per_launch": fl}
+            # HBM bytes per launch of the same call from the committed rocprofv3 PMC passes
+            # (profiles/pmc_traffic.py), when they were taken on this call
+            tpath = os.path.join(ROOT, "profiles", f"{args.config}_traffic.json")
+            if os.path.exists(tpath):
+                try:
+                    t = json.load(open(tpath))["calls"].get(label.split(":")[0])
+                    if t is not None:
+                        roof["traffic"] = round(float(t["traffic_bytes"]))
+                except (OSError, ValueError, KeyError):
+                    pass
         step_ms_eager = sum(km.values())
         if args.kernel_table and rank == 0:
             with open(args.kernel_table, "w") as fh:

@@ -336,6 +336,7 @@ static int grid_for(long M) {
 int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const float* bias, float* out,
                   const cv_epilogue* ep, hipStream_t st) {
   if (g.cs != 32 || g.kh != g.kw || (g.kh != 3 && g.kh != 4) || (g.cb != 1 && g.cb != 3)) return -1;
+  if (g.kh * g.kw * g.cb > 16) return -1;  // K = 48 (3-channel 4x4) is a real contraction: MFMA igemm
   if (in->xf != CV_XF_NONE) CV_REQUIRE(in->bn.C == g.cb, "narrow_gather: BN width %d != %d", in->bn.C, g.cb);
   if (check_ep(ep, g.cs, "narrow_gather")) return 1;
   NArgs a;

@@ -19,10 +19,14 @@ no host writes.  Host-visible PyTorch state (param .data / .grad, optimizer.stat
 exp_avg_sq, BN running stats) are views of, or are updated in place by, the same device buffers;
 the optimizer's CPU 'step' counters are synchronised at the end of every epoch (sync_host_state).
 
-Data parallel: when torch.distributed is initialised with world_size > 1 the gradient arena is
-all-reduced (RCCL over xGMI) between the backward graph and the Adam graph, in two buckets so the
-decoder bucket (ready first) overlaps the encoder backward on a side stream.  Semantics are those
-of torch DDP around the reference (local-batch BN / contrastive / MI terms, averaged gradients).
+Data parallel (cvhip/dist.py): when torch.distributed is initialised with world_size > 1, rank 0's
+parameters are broadcast once, and each step is split into graph segments with the gradient
+all-reduce (RCCL over xGMI, SUM, scaled by 1/world inside the Adam kernel) between them: the
+decoder bucket is launched asynchronously as soon as the decoder backward segment has run, so it
+overlaps the latent + encoder backward segment; the encoder bucket follows and the Adam segment
+waits for both.  In CLEAR-MIM each of the 5 estimator updates all-reduces the estimator gradient
+between its gradient and Adam segments.  Semantics are those of torch DDP around the reference
+(local-batch BN / contrastive / MI terms, averaged gradients).
 """
 
 from __future__ import annotations
@@ -33,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib, rng
+from . import dist as cvdist
 from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
 from .autograd import est_params, mlp_struct
 from .plan import ParamArena, Program, Workspace, ensure_arena, pack_program
@@ -160,6 +165,14 @@ class ClearStep:
             self.est_adam = _AdamState(trainer.mi_estimator_optimizer, self.est_arena)
             self.kind = MI_CLUBSAMPLE if type(self.est).__name__ == "CLUBSample" else MI_L1OUT
             self.learn = torch.zeros(5, dtype=torch.float32, device=self.device)
+        if self.world > 1:  # DDP construction semantics: every rank starts from rank 0's weights
+            cvdist.broadcast_flat(self.arena.flat)
+            if mode == "mim":
+                cvdist.broadcast_flat(self.est_arena.flat)
+            split = self._bucket_split()
+            self.buckets = cvdist.GradBuckets(self.arena.grad, [(split, self.arena.numel), (0, split)])
+            if mode == "mim":
+                self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)])
         # grads visible through p.grad (like the reference after loss.backward())
         for p in self.arena.params:
             p.grad = self.arena.gview(p)
@@ -299,7 +312,31 @@ class ClearStep:
                            E.numel, self.est_adam.hyper, self.est_adam.step)
                 return lp
 
-            learn, learn_inj = make_learn(False), make_learn(True)
+            def make_learn_dp(inject: bool):
+                # per estimator update: (forward + learning-loss gradients, Adam) with the estimator
+                # gradient all-reduced in between
+                out = []
+                for j in range(5):
+                    gp = Program()
+                    if j == 0:
+                        pack_program(sp, gp, "all")
+                    gp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+                    ws.encoder_program(gp, X, True)
+                    ws.reparam_program(gp, eps_buf[1 + j] if inject else None, self.seed, self.offset)
+                    ws.decoder_program(gp, ws.z, True, "none")
+                    ws.running_program(gp, "all")
+                    gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n,
+                           self.learn.data_ptr() + 4 * j, G, None, None, None, None, 0, None, None)
+                    ap = Program()
+                    ap.add("cv_adam_step", E.flat, E.grad, self.est_adam.m, self.est_adam.v, E.numel,
+                           self.est_adam.hyper, self.est_adam.step, self.gscale, None)
+                    out.append((gp, ap))
+                return out
+
+            if self.world > 1:
+                learn, learn_inj = make_learn_dp(False), make_learn_dp(True)
+            else:
+                learn, learn_inj = make_learn(False), make_learn(True)
         return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, upd=upd, learn=learn,
                     fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf)
 
@@ -308,16 +345,45 @@ class ClearStep:
         sp = self.spec
         return self.arena.offset[id(sp.dec_lin.weight)][0]
 
-    def _run_eager(self, G, inject=False):
+    def _segments(self, G, inject=False):
+        """The step as ('prog', [Program...]) segments and ('ar', bucket) / ('ar_est',) / ('wait',)
+        points (single GPU: one segment)."""
+        fwd = G["fwd_inj" if inject else "fwd"]
+        lat = G["lat_inj" if inject else "lat"]
+        learn = G["learn_inj" if inject else "learn"]
+        if self.world == 1:
+            progs = [fwd, G["dec"], lat, G["enc"], G["upd"]] + ([learn] if learn is not None else [])
+            return [("prog", progs)]
+        seg = [("prog", [fwd, G["dec"]]), ("ar", 0), ("prog", [lat, G["enc"]]), ("ar", 1), ("wait",),
+               ("prog", [G["upd"]])]
+        if learn is not None:
+            for gp, ap in learn:
+                seg += [("prog", [gp]), ("ar_est",), ("wait_est",), ("prog", [ap])]
+        return seg
+
+    def _run_segments(self, segs, graphs=None):
         s = _lib.stream_handle()
-        G["fwd_inj" if inject else "fwd"].run(s)
-        G["dec"].run(s)
-        G["lat_inj" if inject else "lat"].run(s)
-        G["enc"].run(s)
-        self._reduce()
-        G["upd"].run(s)
-        if G["learn"] is not None:
-            G["learn_inj" if inject else "learn"].run(s)
+        gi = 0
+        for item in segs:
+            kind = item[0]
+            if kind == "prog":
+                if graphs is None:
+                    for P in item[1]:
+                        P.run(s)
+                else:
+                    graphs[gi].replay()
+                    gi += 1
+            elif kind == "ar":
+                self.buckets.launch(item[1])
+            elif kind == "wait":
+                self.buckets.wait()
+            elif kind == "ar_est":
+                self.est_buckets.launch(0)
+            elif kind == "wait_est":
+                self.est_buckets.wait()
+
+    def _run_eager(self, G, inject=False):
+        self._run_segments(self._segments(G, inject))
 
     def _take_injections(self, G) -> bool:
         """Consume queued test noise (cvhip.rng): eps_c, eps_s for the main forward and, in CLEAR-MIM,
@@ -337,34 +403,18 @@ class ClearStep:
             G["perm_buf"].copy_(pm)
         return True
 
-    def _reduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.arena.grad)
-
     def _capture(self, G):
-        if self.world == 1:
+        graphs = []
+        for item in self._segments(G, False):
+            if item[0] != "prog":
+                continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 s = _lib.stream_handle()
-                for k in ("fwd", "dec", "lat", "enc", "upd"):
-                    G[k].run(s)
-                if G["learn"] is not None:
-                    G["learn"].run(s)
-            G["graphs"] = [g]
-        else:
-            # backward graph / [all-reduce] / update graph
-            g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                s = _lib.stream_handle()
-                for k in ("fwd", "dec", "lat", "enc"):
-                    G[k].run(s)
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
-                s = _lib.stream_handle()
-                G["upd"].run(s)
-                if G["learn"] is not None:
-                    G["learn"].run(s)
-            G["graphs"] = [g1, g2]
+                for P in item[1]:
+                    P.run(s)
+            graphs.append(g)
+        G["graphs"] = graphs
 
     # ----------------------------------------------------------------------------- one step
     def step(self, X, label):
@@ -384,12 +434,7 @@ class ClearStep:
         if use_graph and "graphs" not in G:
             self._capture(G)
         if use_graph:
-            if self.world == 1:
-                G["graphs"][0].replay()
-            else:
-                G["graphs"][0].replay()
-                self._reduce()
-                G["graphs"][1].replay()
+            self._run_segments(self._segments(G, False), G["graphs"])
         else:
             self._run_eager(G, inject)
         G["count"] += 1

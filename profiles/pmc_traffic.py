@@ -1,0 +1,55 @@
+"""HBM traffic per launch of one step-program call from rocprofv3 PMC passes (MI355X_MICROARCH.md,
+"HBM"): FETCH_SIZE and WRITE_SIZE are collected in SEPARATE passes (they do not fit one TCC pass),
+each run as
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir>/fetch -o run -- \
+        python bench.py --only-call 'enc[4]' --reps 50 --warmup 5 --no-cpu-baseline --no-kernel-pass
+    rocprofv3 --pmc WRITE_SIZE ... -d <dir>/write ...
+
+FETCH_SIZE is in KiB and on gfx950 counts half the bytes of 16-B-per-lane streaming reads (128-B
+requests tallied at 64 B), so it is doubled; WRITE_SIZE (KiB) is exact for 16-B stores and float
+atomics.  The per-launch figure is the median over the last --reps dispatches of the call's dominant
+kernel (the warmup steps dispatch the same kernel for other layers first).
+
+    python profiles/pmc_traffic.py <dir> 'enc[4]' <kernel-name-substring> <reps> <out.json>   (merges)
+"""
+
+import csv
+import glob
+import json
+import statistics
+import sys
+
+
+def per_dispatch(path_glob, counter, kernel_sub):
+    vals = {}
+    for path in glob.glob(path_glob, recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name") != counter or kernel_sub not in r.get("Kernel_Name", ""):
+                continue
+            d = int(r["Dispatch_Id"])
+            vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def main():
+    d, call, ksub, reps, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    fetch = per_dispatch(f"{d}/fetch/**/*counter_collection.csv", "FETCH_SIZE", ksub)[-reps:]
+    write = per_dispatch(f"{d}/write/**/*counter_collection.csv", "WRITE_SIZE", ksub)[-reps:]
+    if not fetch or not write:
+        raise SystemExit(f"no dispatches of {ksub!r} found under {d}")
+    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+    rec = {"kernel": ksub, "dispatches": [len(fetch), len(write)],
+           "fetch_size_kib_median": f_kib, "write_size_kib_median": w_kib,
+           "traffic_bytes": 2 * f_kib * 1024 + w_kib * 1024}
+    try:
+        db = json.load(open(out))
+    except (OSError, ValueError):
+        db = {"note": "per launch: traffic = 2*FETCH_SIZE (gfx950 16B-load correction) + WRITE_SIZE", "calls": {}}
+    db["calls"][call] = rec
+    json.dump(db, open(out, "w"), indent=1)
+    print(json.dumps({call: rec}))
+
+
+if __name__ == "__main__":
+    main()
