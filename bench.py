@@ -81,8 +81,12 @@ def kernel_pass(engine, G, reps=20, rounds=3):
     from cvhip import _lib
 
     progs = [("fwd", G["fwd"]), ("dec", G["dec"]), ("lat", G["lat"]), ("enc", G["enc"]), ("upd", G["upd"])]
-    if G.get("learn") is not None:
-        progs.append(("learn", G["learn"]))
+    learn = G.get("learn")
+    if isinstance(learn, list):  # data-parallel CLEAR-MIM: (gradient, Adam) program pairs
+        for j, (gp, ap) in enumerate(learn):
+            progs += [(f"learn{j}g", gp), (f"learn{j}a", ap)]
+    elif learn is not None:
+        progs.append(("learn", learn))
     times = {}
     for pname, P in progs:
         for i, (name, fn, args) in enumerate(P.calls):
@@ -112,6 +116,8 @@ def gemm_flops_of(label, G, engine):
     """Algorithmic FLOPs of one igemm call from its program position (conv / linear layers)."""
     pname, rest = label.split("[", 1)
     idx = int(rest.split("]")[0])
+    if not hasattr(G.get(pname), "calls"):
+        return None
     name, fn, args = G[pname].calls[idx]
     if name.startswith("cv_conv_"):
         g = args[0]._obj

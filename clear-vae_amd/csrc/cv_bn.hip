@@ -91,46 +91,65 @@ __global__ __launch_bounds__(256) void output_fwd_kernel(const cv_bn b, const fl
 
 // Fused output + reconstruction loss + backward seed.  Elements are visited in NHWC order so the
 // dv store (NHWC) is coalesced; x / xhat are NCHW.
+// grid-stride over element batches of OL_U per thread: all loads of a batch are issued first
+constexpr int OL_U = 4;
 __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const float* __restrict__ y,
                                                           const float* __restrict__ x, int n, int c, int hw,
+                                                          const FDiv fc, const FDiv fhw,
                                                           float* __restrict__ xhat, double* rec_out,
                                                           float* __restrict__ dv, double* gstat,
                                                           const float* rec_scale) {
   __shared__ BnFwdC k[OUT_MAXC];
-  __shared__ float2 mi[OUT_MAXC];
   __shared__ double red[4][1 + 2 * OUT_MAXC];
   __shared__ double scratch[4 * 256];
-  bn_fold<256>(b, false, scratch, [&](int f, double s, double q, double, double) {
-    k[f] = bn_fwd_const_s(b, f, s, q);
-    mi[f] = make_float2(k[f].mu, k[f].istd);
-  });
+  bn_fold<256>(b, false, scratch, [&](int f, double s, double q, double, double) { k[f] = bn_fwd_const_s(b, f, s, q); });
   const float scale = (rec_scale ? rec_scale[0] : 1.0f) * 2.0f / (float)n;
-  const long total = (long)n * c * hw;
+  const int total = n * c * hw;
   float rec = 0.f;
   float s1[OUT_MAXC], s2[OUT_MAXC];
 #pragma unroll
   for (int j = 0; j < OUT_MAXC; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int ch = (int)(i % c);
-    const long pix = i / c;  // img*hw + p
-    const long img = pix / hw;
-    const int p = (int)(pix - img * hw);
-    const long nchw = (img * c + ch) * hw + p;
-    const float yv = y[i];
-    const float v = bn_out(yv, k[ch]);
-    const float xh = 1.0f / (1.0f + expf(-v));
-    const float diff = xh - x[nchw];
-    xhat[nchw] = xh;
-    rec = fmaf(diff, diff, rec);
-    if (dv) {
-      const float d = scale * diff * xh * (1.0f - xh);
-      dv[i] = d;
+  for (int base = blockIdx.x * 256 * OL_U; base < total; base += gridDim.x * 256 * OL_U) {
+    float yv[OL_U], xv[OL_U];
+    int nchw[OL_U], chs[OL_U];
 #pragma unroll
-      for (int j = 0; j < OUT_MAXC; ++j)
-        if (j == ch) {
-          s1[j] += d;
-          s2[j] += d * ((yv - mi[ch].x) * mi[ch].y);
-        }
+    for (int u = 0; u < OL_U; ++u) {
+      const int i = base + u * 256 + threadIdx.x;
+      yv[u] = 0.f;
+      xv[u] = 0.f;
+      nchw[u] = -1;
+      chs[u] = 0;
+      if (i < total) {
+        const int pix = fc.div(i);  // img*hw + p
+        const int ch = i - pix * c;
+        const int img = fhw.div(pix);
+        const int p = pix - img * hw;
+        nchw[u] = (img * c + ch) * hw + p;
+        chs[u] = ch;
+        yv[u] = y[i];
+        xv[u] = x[nchw[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < OL_U; ++u) {
+      if (nchw[u] < 0) continue;
+      const int ch = chs[u];
+      const BnFwdC kk = k[ch];
+      const float v = bn_out(yv[u], kk);
+      const float xh = 1.0f / (1.0f + expf(-v));
+      const float diff = xh - xv[u];
+      xhat[nchw[u]] = xh;
+      rec = fmaf(diff, diff, rec);
+      if (dv) {
+        const float d = scale * diff * xh * (1.0f - xh);
+        dv[base + u * 256 + threadIdx.x] = d;
+#pragma unroll
+        for (int j = 0; j < OUT_MAXC; ++j)
+          if (j == ch) {
+            s1[j] += d;
+            s2[j] += d * ((yv[u] - kk.mu) * kk.istd);
+          }
+      }
     }
   }
   // block reduction (fp64 for the outputs)
@@ -147,7 +166,7 @@ __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const f
   __syncthreads();
   if (threadIdx.x == 0) {
     double r = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-    atomic_add_f64(rec_out, r / (double)n);
+    atomic_add_f64(rec_out + blockIdx.x % CV_REC_REPL, r / (double)n);
     if (dv) {
       const int repl = blockIdx.x % CV_STAT_REPL(c);
       for (int j = 0; j < c; ++j) {
@@ -212,7 +231,7 @@ __global__ __launch_bounds__(256) void output_bwd_kernel(const cv_bn b, const fl
 
 // BN1d(+ReLU) applied elementwise; the tensor is stored in the Unflatten/NHWC order.  Thread =
 // one storage column (constants computed once), looping over a chunk of rows: coalesced rows.
-constexpr int BA_ROWS = 8;
+constexpr int BA_ROWS = 32;
 __global__ __launch_bounds__(256) void bn_apply_kernel(const cv_bn b, const float* __restrict__ x,
                                                        float* __restrict__ out, int rows, int F, int pix, int ch,
                                                        int relu) {
@@ -221,10 +240,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const cv_bn b, const floa
   const int f = (pix > 1) ? (col % ch) * pix + col / ch : col;  // PyTorch feature c*pix + p
   const BnFwdC k = bn_fwd_const(b, f);
   const int r0 = blockIdx.y * BA_ROWS;
-  for (int r = r0; r < min(rows, r0 + BA_ROWS); ++r) {
-    const size_t i = (size_t)r * F + col;
-    const float v = bn_out(x[i], k);
-    out[i] = relu ? fmaxf(v, 0.f) : v;
+  constexpr int U = 8;
+  for (int rb = r0; rb < min(rows, r0 + BA_ROWS); rb += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = (rb + u < rows) ? x[(size_t)(rb + u) * F + col] : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (rb + u >= rows) break;
+      const float o = bn_out(v[u], k);
+      out[(size_t)(rb + u) * F + col] = relu ? fmaxf(o, 0.f) : o;
+    }
   }
 }
 
@@ -241,40 +267,62 @@ static int elem_grid(long total) {
 constexpr int DL_F = 64;
 constexpr int DL_R = 64;
 
+// Both kernels walk the activation in its storage (Unflatten / NHWC) order so loads are coalesced;
+// storage column col holds PyTorch feature f(col) = (col % ch) * pix + col / ch.
+__device__ __forceinline__ int dl_feature(int col, int pix, int ch) {
+  if (pix <= 1) return col;
+  const int p = col / ch;
+  return (col - p * ch) * pix + p;
+}
+
+constexpr int DL_RPT = DL_R / 4;  // rows per thread (4 row groups per block)
+
 __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int pix, int ch, float* da,
                                                              const float* __restrict__ h, const cv_bn b,
                                                              double* gstat) {
   __shared__ float r1[4][DL_F], r2[4][DL_F];
-  __shared__ BnFwdC kf[DL_F];
+  __shared__ int fidx[DL_F];
   const int t = threadIdx.x;
-  const int f0 = blockIdx.x * DL_F, rbase = blockIdx.y * DL_R;
-  if (t < DL_F && f0 + t < F) kf[t] = bn_fwd_const(b, f0 + t);
-  __syncthreads();
-  const int fl = t % DL_F, rg = t / DL_F;
-  const int f = f0 + fl;
-  float s1 = 0.f, s2 = 0.f;
-  if (f < F) {
-    const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
-    const BnFwdC k = kf[fl];
-    for (int r = rbase + rg; r < min(n, rbase + DL_R); r += 4) {
-      const size_t off = (size_t)r * F + col;
-      const float hv = h[off];
-      float d = da[off];
-      if (bn_out(hv, k) <= 0.f) d = 0.f;
-      da[off] = d;
-      s1 += d;
-      s2 += d * ((hv - k.mu) * k.istd);
+  const int c0 = blockIdx.x * DL_F, rbase = blockIdx.y * DL_R;
+  const int cl = t % DL_F, rg = t / DL_F;
+  const int col = c0 + cl;
+  const int f = col < F ? dl_feature(col, pix, ch) : 0;
+  BnFwdC k;
+  if (col < F) k = bn_fwd_const(b, f);
+  float hv[DL_RPT], dv[DL_RPT];
+#pragma unroll
+  for (int i = 0; i < DL_RPT; ++i) {  // issue every load of the column slice first
+    const int r = rbase + rg + 4 * i;
+    hv[i] = 0.f;
+    dv[i] = 0.f;
+    if (col < F && r < n) {
+      hv[i] = h[(size_t)r * F + col];
+      dv[i] = da[(size_t)r * F + col];
     }
   }
-  r1[rg][fl] = s1;
-  r2[rg][fl] = s2;
+  float s1 = 0.f, s2 = 0.f;
+  if (col < F) {
+#pragma unroll
+    for (int i = 0; i < DL_RPT; ++i) {
+      const int r = rbase + rg + 4 * i;
+      if (r >= n) continue;
+      float d = dv[i];
+      if (bn_out(hv[i], k) <= 0.f) d = 0.f;
+      da[(size_t)r * F + col] = d;
+      s1 += d;
+      s2 += d * ((hv[i] - k.mu) * k.istd);
+    }
+  }
+  r1[rg][cl] = s1;
+  r2[rg][cl] = s2;
+  if (rg == 0) fidx[cl] = f;
   __syncthreads();
-  if (t < DL_F && f0 + t < F) {
+  if (t < DL_F && c0 + t < F) {
     const double a = (double)r1[0][t] + r1[1][t] + r1[2][t] + r1[3][t];
     const double q = (double)r2[0][t] + r2[1][t] + r2[2][t] + r2[3][t];
     const int repl = (blockIdx.y * gridDim.x + blockIdx.x) % CV_STAT_REPL(F);
-    atomic_add_f64(gstat + (size_t)repl * 2 * F + f0 + t, a);
-    atomic_add_f64(gstat + (size_t)repl * 2 * F + F + f0 + t, q);
+    atomic_add_f64(gstat + (size_t)repl * 2 * F + fidx[t], a);
+    atomic_add_f64(gstat + (size_t)repl * 2 * F + F + fidx[t], q);
   }
 }
 
@@ -285,43 +333,58 @@ __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int 
                                                               const float* __restrict__ z, float* gw) {
   __shared__ float sd[DL_R][DL_F + 1];
   __shared__ float sz[DL_R][4 * KPT + 1];
-  __shared__ BnBwdC kb[DL_F];
   const int t = threadIdx.x;
-  const int f0 = blockIdx.x * DL_F, r0 = blockIdx.y * DL_R;
-  if (t < DL_F && f0 + t < F) kb[t] = bn_bwd_const(b, f0 + t);
-  __syncthreads();
-  for (int e = t; e < DL_R * DL_F; e += 256) {
-    const int rr = e / DL_F, ff = e % DL_F;
-    const int r = r0 + rr, f = f0 + ff;
-    float v = 0.f;
-    if (r < n && f < F) {
-      const int col = (pix > 1) ? (f % pix) * ch + f / pix : f;
-      const size_t off = (size_t)r * F + col;
-      v = bn_bwd(dz[off], h[off], kb[ff]);
+  const int c0 = blockIdx.x * DL_F, r0 = blockIdx.y * DL_R;
+  const int cl = t % DL_F, rg = t / DL_F;
+  const int col = c0 + cl;
+  const int f = col < F ? dl_feature(col, pix, ch) : 0;
+  BnBwdC kb;
+  if (col < F) kb = bn_bwd_const(b, f);
+  float dv[DL_RPT], hv[DL_RPT];
+#pragma unroll
+  for (int i = 0; i < DL_RPT; ++i) {
+    const int r = r0 + rg + 4 * i;
+    dv[i] = 0.f;
+    hv[i] = 0.f;
+    if (col < F && r < n) {
+      dv[i] = dz[(size_t)r * F + col];
+      hv[i] = h[(size_t)r * F + col];
     }
-    sd[rr][ff] = v;
   }
-  for (int e = t; e < DL_R * K; e += 256) {
-    const int rr = e / K, kk = e % K;
-    const int r = r0 + rr;
-    sz[rr][kk] = (r < n) ? z[(size_t)r * K + kk] : 0.f;
+  constexpr int ZPT = (DL_R * 4 * KPT + 255) / 256;
+  float zv[ZPT];
+#pragma unroll
+  for (int j = 0; j < ZPT; ++j) {
+    const int e = t + 256 * j;
+    const int rr = e / (4 * KPT), kk = e % (4 * KPT);
+    zv[j] = (e < DL_R * 4 * KPT && r0 + rr < n && kk < K) ? z[(size_t)(r0 + rr) * K + kk] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < DL_RPT; ++i) {
+    const int r = r0 + rg + 4 * i;
+    sd[rg + 4 * i][cl] = (col < F && r < n) ? bn_bwd(dv[i], hv[i], kb) : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < ZPT; ++j) {
+    const int e = t + 256 * j;
+    if (e < DL_R * 4 * KPT) sz[e / (4 * KPT)][e % (4 * KPT)] = zv[j];
   }
   __syncthreads();
-  const int fl = t % DL_F, kg = t / DL_F;
+  const int kg = rg;
   float acc[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) acc[j] = 0.f;
   const int rmax = min(DL_R, n - r0);
   for (int rr = 0; rr < rmax; ++rr) {
-    const float dv = sd[rr][fl];
+    const float d = sd[rr][cl];
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) acc[j] = fmaf(dv, sz[rr][kg + 4 * j], acc[j]);
+    for (int j = 0; j < KPT; ++j) acc[j] = fmaf(d, sz[rr][kg + 4 * j], acc[j]);
   }
-  if (f0 + fl < F) {
+  if (col < F) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
       const int kk = kg + 4 * j;
-      if (kk < K) atomicAdd(gw + (size_t)(f0 + fl) * K + kk, acc[j]);
+      if (kk < K) atomicAdd(gw + (size_t)f * K + kk, acc[j]);
     }
   }
 }
@@ -410,8 +473,11 @@ extern "C" int cv_output_loss(const cv_bn* bn, const float* y, const float* x, i
              "output_loss: bad args (C<=%d)", OUT_MAXC);
   CV_REQUIRE(bn->C == c, "output_loss: BN width %d != %d", bn->C, c);
   CV_REQUIRE(!dv_out || gstat_out, "output_loss: dv needs gstat_out");
-  hipLaunchKernelGGL(output_loss_kernel, dim3(elem_grid((long)n * c * hw)), dim3(256), 0, S(stream), *bn, y, x, n, c,
-                     hw, xhat, rec_out, dv_out, gstat_out, rec_scale);
+  CV_REQUIRE((long)n * c * hw < (1L << 31), "output_loss: tensor too large");
+  long g = ((long)n * c * hw + 256 * OL_U - 1) / (256 * OL_U);
+  if (g > 512) g = 512;
+  hipLaunchKernelGGL(output_loss_kernel, dim3((int)g), dim3(256), 0, S(stream), *bn, y, x, n, c, hw, FDiv::make(c),
+                     FDiv::make(hw), xhat, rec_out, dv_out, gstat_out, rec_scale);
   CV_LAUNCH_CHECK("output_loss");
   return 0;
 }

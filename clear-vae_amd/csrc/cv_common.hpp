@@ -35,6 +35,27 @@ void clear_error();
 static inline hipStream_t S(cv_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Division by a runtime-invariant divisor as multiply-high + add + shift ("division by invariant
+// integers"): valid for 0 <= n < 2^31.  The igemm hot loops divide by channel / tap / pixel counts
+// per K tile; as v_div sequences those were ~20x the MFMA instruction count (PMC SQ_INSTS_VALU).
+struct FDiv {
+  uint32_t d, m, s;
+  __host__ __device__ static FDiv make(uint32_t d) {
+    FDiv f;
+    f.d = d < 1 ? 1 : d;
+    uint32_t s = 0;
+    while ((1ull << s) < f.d) ++s;
+    f.s = s;
+    f.m = (uint32_t)((((1ull << 32) * ((1ull << s) - f.d)) / f.d) + 1);
+    return f;
+  }
+  __device__ __forceinline__ int div(int n) const {
+    const uint32_t t = __umulhi((uint32_t)n, m);
+    return (int)((t + (uint32_t)n) >> s);
+  }
+  __device__ __forceinline__ int mod(int n) const { return n - div(n) * (int)d; }
+};
+
 // generic conv geometry: small grid S (hs x ws x cs), big grid B (hb x wb x cb), yb = ys*s - p + kh.
 // Conv2d: small = output, big = input; ConvTranspose2d: small = input, big = output.
 struct Geo {

@@ -27,6 +27,9 @@
 namespace cv {
 
 constexpr int BK = 32;
+#ifndef CV_DEPTH
+#define CV_DEPTH 2  // register-ring depth (tiles staged ahead + 1); 3 measured slower (occupancy)
+#endif
 constexpr int NT = 256;
 
 enum { OP_GATHER = 0, OP_SCATTER = 1, OP_WGRAD = 2, OP_DENSE = 3 };
@@ -51,6 +54,8 @@ struct Args {
   int lda, a_pix, a_ch;      // DENSE: A row stride; NCHW-flatten permutation of A columns (a_pix=1: none)
   int ldo, o_pix, o_ch;      // DENSE: out row stride; permutation of output columns
   int ca_n, cb_n, ce_n;      // feature counts of a / b / epilogue BN constants (0 = unused)
+  // fast divisors (filled by finalize_divs at launch)
+  FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
 };
 
 // ------------------------------------------------------------------ operand transform helpers
@@ -133,7 +138,10 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   float* Bs = As + 2 * ABUF;            // [2][BBUF]
   float* red = Bs + 2 * BBUF;           // epilogue reduction scratch: 2 * WM * BN floats
   float* cstA = red + 2 * WM * BN;      // BN constants
-  float* cstB = cstA + xf_floats(P.a.xf, P.ca_n);
+  // DENSE with a BatchNorm1d over the K features (decoder Linear backward): constants only for this
+  // block's K chunk, indexed k - kbeg (folding all K features per block was 65k fp64 loads each)
+  const bool bn1d = (OP == OP_DENSE) && P.ca_n == P.K && P.a.xf != CV_XF_NONE;
+  float* cstB = cstA + xf_floats(P.a.xf, bn1d ? P.kchunk : P.ca_n);
   float* cstE = cstB + xf_floats(P.b.xf, P.cb_n);
 
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -162,6 +170,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   const int N = P.N + ((OP == OP_WGRAD && P.gbias) ? 1 : 0);
   int kbeg = 0, kend = K;
   int ry = 0, rx = 0, yb0 = 0, xb0 = 0, cy = 1, cx = 1, ntx = 1;
+  FDiv f_cx = FDiv::make(1), f_cycx = FDiv::make(1), f_ntx = FDiv::make(1);
   if (OP == OP_SCATTER) {
     const int s = g.s, cls = bz;
     ry = cls / s;
@@ -176,6 +185,9 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     K = nty * ntx * g.cs;
     kend = K;
     if (m0 >= M) return;
+    f_cx = FDiv::make(cx);
+    f_cycx = FDiv::make(cy * cx);
+    f_ntx = FDiv::make(ntx);
   } else {
     kbeg = bz * P.kchunk;
     kend = min(K, kbeg + P.kchunk);
@@ -186,7 +198,21 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   double* fold_scratch = reinterpret_cast<double*>(As);
   static_assert(2 * BK * (ROWS ? BM : BM + 16) * sizeof(float) >= 4 * NT * sizeof(double), "fold scratch");
   XfA ca, cb;
-  fill_consts(P.a, P.ca_n, cstA, fold_scratch, ca);
+  if (bn1d) {
+    ca.f = reinterpret_cast<const BnFwdC*>(cstA);
+    ca.bw = reinterpret_cast<const BnBwdC*>(cstA);
+    for (int idx = t; idx < kend - kbeg; idx += NT) {
+      int f = kbeg + idx;
+      if (P.a_pix > 1) {
+        const int pix = f / P.a_ch, c = f - pix * P.a_ch;
+        f = c * P.a_pix + pix;
+      }
+      if (P.a.xf == CV_XF_BNRELU) reinterpret_cast<BnFwdC*>(cstA)[idx] = bn_fwd_const(P.a.bn, f);
+      else reinterpret_cast<BnBwdC*>(cstA)[idx] = bn_bwd_const(P.a.bn, f);
+    }
+  } else {
+    fill_consts(P.a, P.ca_n, cstA, fold_scratch, ca);
+  }
   fill_consts(P.b, P.cb_n, cstB, fold_scratch, cb);
   if (P.ep.stat_mode == CV_STAT_BWD) {
     BnFwdC* d = reinterpret_cast<BnFwdC*>(cstE);
@@ -207,16 +233,16 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
       const int rr = r_ok[i] ? r : 0;
       if (OP == OP_GATHER) {
         const int hw = g.hs * g.ws;
-        r_n[i] = rr / hw;
+        r_n[i] = P.f_hws.div(rr);
         const int rem = rr - r_n[i] * hw;
-        const int ys = rem / g.ws, xs = rem - ys * g.ws;
+        const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
         r_y[i] = ys * g.s - g.p;  // big-grid origin of the receptive field
         r_x[i] = xs * g.s - g.p;
       } else if (OP == OP_SCATTER) {
         const int hw = cy * cx;
-        r_n[i] = rr / hw;
+        r_n[i] = f_cycx.div(rr);
         const int rem = rr - r_n[i] * hw;
-        const int ty = rem / cx, tx = rem - ty * cx;
+        const int ty = f_cx.div(rem), tx = rem - ty * cx;
         r_y[i] = yb0 + g.s * ty + g.p;  // (yb + p); ys = (r_y - kh) / s
         r_x[i] = xb0 + g.s * tx + g.p;
       } else {
@@ -236,68 +262,71 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   const bool b_vec = (OP == OP_WGRAD) && (g.cb & 3) == 0 && !P.b.nchw;
   const bool a_bwd = P.a.xf == CV_XF_BNBWD, b_bwd = P.b.xf == CV_XF_BNBWD;
 
-  float4 ra[RAW], rya[RAW];
-  float4 rb[BW], ryb[BW];
-  unsigned amask = 0, bmask = 0;
+  // one register stage of a K tile (raw operand values, BN-backward partners, validity masks)
+  struct Stage {
+    float4 ra[RAW], rya[RAW];
+    float4 rb[BW], ryb[BW];
+    unsigned amask, bmask;
+  };
 
   // DENSE: the K loop runs in the storage order of A (k' = pix*a_ch + c for an NCHW-flattened
   // input); lf() is the PyTorch feature index of k' (weight column / BN1d feature)
   auto lf = [&](int kk) -> int {
     if (P.a_pix <= 1) return kk;
-    const int pix = kk / P.a_ch, c = kk - pix * P.a_ch;
+    const int pix = P.f_ach.div(kk), c = kk - pix * P.a_ch;
     return c * P.a_pix + pix;
   };
 
   // ---------------- A: fetch raw values into registers
-  auto fetchA = [&](int k0) {
-    amask = 0;
+  auto fetchA = [&](Stage& S, int k0) {
+    S.amask = 0;
     if (ROWS) {
       const int kq = k0 + 4 * quad;
       if (a_vec) {
         if (OP == OP_GATHER) {
-          const int tap = kq / g.cb, c0 = kq - tap * g.cb;
-          const int kh = tap / g.kw, kw = tap - kh * g.kw;
+          const int tap = P.f_cb.div(kq), c0 = kq - tap * g.cb;
+          const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
 #pragma unroll
           for (int i = 0; i < RA; ++i) {
             const int yb = r_y[i] + kh, xb = r_x[i] + kw;
-            ra[i] = z4();
-            rya[i] = z4();
+            S.ra[i] = z4();
+            S.rya[i] = z4();
             if (r_ok[i] && kq < kend && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
               const size_t off = ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
-              ra[i] = ld4(P.a.x + off);
-              if (a_bwd) rya[i] = ld4(P.a.y + off);
-              amask |= 1u << i;
+              S.ra[i] = ld4(P.a.x + off);
+              if (a_bwd) S.rya[i] = ld4(P.a.y + off);
+              S.amask |= 1u << i;
             }
           }
         } else if (OP == OP_SCATTER) {
-          const int tap = kq / g.cs, c0 = kq - tap * g.cs;
-          const int jy = tap / ntx, jx = tap - jy * ntx;
+          const int tap = P.f_cs.div(kq), c0 = kq - tap * g.cs;
+          const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
           const int kh = ry + g.s * jy, kw = rx + g.s * jx;
 #pragma unroll
           for (int i = 0; i < RA; ++i) {
             const int py = r_y[i] - kh, px = r_x[i] - kw;  // divisible by s by construction
-            ra[i] = z4();
-            rya[i] = z4();
+            S.ra[i] = z4();
+            S.rya[i] = z4();
             if (r_ok[i] && kq < kend && py >= 0 && px >= 0) {
-              const int ys = py / g.s, xs = px / g.s;
+              const int ys = P.f_s.div(py), xs = P.f_s.div(px);
               if (ys < g.hs && xs < g.ws) {
                 const size_t off = ((size_t)(r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c0;
-                ra[i] = ld4(P.a.x + off);
-                if (a_bwd) rya[i] = ld4(P.a.y + off);
-                amask |= 1u << i;
+                S.ra[i] = ld4(P.a.x + off);
+                if (a_bwd) S.rya[i] = ld4(P.a.y + off);
+                S.amask |= 1u << i;
               }
             }
           }
         } else {  // DENSE, storage-order k'
 #pragma unroll
           for (int i = 0; i < RA; ++i) {
-            ra[i] = z4();
-            rya[i] = z4();
+            S.ra[i] = z4();
+            S.rya[i] = z4();
             if (r_ok[i] && kq < kend) {
               const size_t off = (size_t)r_n[i] * P.lda + kq;
-              ra[i] = ld4(P.a.x + off);
-              if (a_bwd) rya[i] = ld4(P.a.y + off);
-              amask |= 1u << i;
+              S.ra[i] = ld4(P.a.x + off);
+              if (a_bwd) S.rya[i] = ld4(P.a.y + off);
+              S.amask |= 1u << i;
             }
           }
         }
@@ -314,31 +343,31 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
             int ch;
             bool ok = true;
             if (OP == OP_GATHER) {
-              const int tap = k / g.cb, c = k - tap * g.cb;
-              const int kh = tap / g.kw, kw = tap - kh * g.kw;
+              const int tap = P.f_cb.div(k), c = k - tap * g.cb;
+              const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
               const int yb = r_y[i] + kh, xb = r_x[i] + kw;
               ok = (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
               off = P.a.nchw ? ((size_t)(r_n[i] * g.cb + c) * g.hb + yb) * g.wb + xb
                              : ((size_t)(r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c;
               ch = c;
             } else if (OP == OP_SCATTER) {
-              const int tap = k / g.cs, c = k - tap * g.cs;
-              const int jy = tap / ntx, jx = tap - jy * ntx;
+              const int tap = P.f_cs.div(k), c = k - tap * g.cs;
+              const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
               const int py = r_y[i] - (ry + g.s * jy), px = r_x[i] - (rx + g.s * jx);
-              ok = py >= 0 && px >= 0 && py / g.s < g.hs && px / g.s < g.ws;
-              off = ((size_t)(r_n[i] * g.hs + (ok ? py / g.s : 0)) * g.ws + (ok ? px / g.s : 0)) * g.cs + c;
+              ok = py >= 0 && px >= 0 && P.f_s.div(py) < g.hs && P.f_s.div(px) < g.ws;
+              off = ((size_t)(r_n[i] * g.hs + (ok ? P.f_s.div(py) : 0)) * g.ws + (ok ? P.f_s.div(px) : 0)) * g.cs + c;
               ch = c;
             } else {
               off = (size_t)r_n[i] * P.lda + k;
               const int f = lf(k);
-              ch = (P.ca_n == P.K) ? f : (P.a_pix > 1 ? k % P.a_ch : f);
+              ch = bn1d ? k - kbeg : (P.a_pix > 1 ? P.f_ach.mod(k) : f);
             }
             if (ok) {
               const float yv = a_bwd ? P.a.y[off] : 0.f;
               tmp[j] = xf_apply(P.a, ca, ch, P.a.x[off], yv);
             }
           }
-          ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+          S.ra[i] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         }
       }
     } else {  // WGRAD A(m = cs, k = small pixel): float4 along cs
@@ -348,15 +377,15 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
         const int pix = k0 + kk, c0 = m0 + 4 * mq;
-        ra[e] = z4();
-        rya[e] = z4();
+        S.ra[e] = z4();
+        S.rya[e] = z4();
         if (kk < BK && pix < kend) {
           const size_t off = (size_t)pix * g.cs + c0;
           if (a_vec) {
             if (c0 < g.cs) {
-              ra[e] = ld4(P.a.x + off);
-              if (a_bwd) rya[e] = ld4(P.a.y + off);
-              amask |= 1u << e;
+              S.ra[e] = ld4(P.a.x + off);
+              if (a_bwd) S.rya[e] = ld4(P.a.y + off);
+              S.amask |= 1u << e;
             }
           } else {
             float tmp[4];
@@ -368,7 +397,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
                 tmp[j] = xf_apply(P.a, ca, c0 + j, P.a.x[off + j], yv);
               }
             }
-            ra[e] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+            S.ra[e] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
         }
       }
@@ -376,29 +405,24 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   };
 
   // ---------------- A: transform (vector paths) + store to LDS
-  auto storeA = [&](float* Ab, int k0) {
+  auto storeA = [&](Stage& S, float* Ab, int k0) {
     if (ROWS) {
       const int kq = k0 + 4 * quad;
       int ch0 = 0;
       if (a_vec && P.a.xf != CV_XF_NONE) {
-        if (OP == OP_GATHER) ch0 = kq % g.cb;
-        else if (OP == OP_SCATTER) ch0 = kq % g.cs;
-        else ch0 = (P.a_pix > 1) ? kq % P.a_ch : kq;
+        if (OP == OP_GATHER) ch0 = P.f_cb.mod(kq);
+        else if (OP == OP_SCATTER) ch0 = P.f_cs.mod(kq);
+        else ch0 = (P.a_pix > 1) ? P.f_ach.mod(kq) : kq;
       }
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
-        float4 v = ra[i];
+        float4 v = S.ra[i];
         if (a_vec && P.a.xf != CV_XF_NONE) {
-          if (amask & (1u << i)) {
-            if (OP == OP_DENSE && P.a_pix > 1 && P.ca_n == P.K) {  // BN1d over NCHW-order features
-              const int pix = kq / P.a_ch;
-              float vv[4] = {v.x, v.y, v.z, v.w};
-              const float yy[4] = {rya[i].x, rya[i].y, rya[i].z, rya[i].w};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) vv[e] = xf_apply(P.a, ca, (ch0 + e) * P.a_pix + pix, vv[e], yy[e]);
-              v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+          if (S.amask & (1u << i)) {
+            if (bn1d) {  // BN1d: constants of this block's K chunk, in k order
+              v = xf_apply4(P.a, ca, kq - kbeg, v, S.rya[i]);
             } else {
-              v = xf_apply4(P.a, ca, ch0, v, rya[i]);
+              v = xf_apply4(P.a, ca, ch0, v, S.rya[i]);
             }
           }
         }
@@ -411,8 +435,8 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
       for (int e = 0; e < AW; ++e) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
-        float4 v = ra[e];
-        if (a_vec && P.a.xf != CV_XF_NONE && (amask & (1u << e))) v = xf_apply4(P.a, ca, m0 + 4 * mq, v, rya[e]);
+        float4 v = S.ra[e];
+        if (a_vec && P.a.xf != CV_XF_NONE && (S.amask & (1u << e))) v = xf_apply4(P.a, ca, m0 + 4 * mq, v, S.rya[e]);
         if (kk < BK) *reinterpret_cast<float4*>(Ab + kk * LDA + 4 * mq) = v;
       }
     }
@@ -420,15 +444,15 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
 
   // ---------------- B: one float4 of a K row (4 consecutive columns) per slot
   constexpr int NQ = BN / 4;
-  auto fetchB = [&](int k0) {
-    bmask = 0;
+  auto fetchB = [&](Stage& S, int k0) {
+    S.bmask = 0;
 #pragma unroll
     for (int e = 0; e < BW; ++e) {
       const int idx = t + NT * e;
       const int nq = idx % NQ, kk = idx / NQ;
       const int col = n0 + 4 * nq, k = k0 + kk;
       float4 v = z4();
-      ryb[e] = z4();
+      S.ryb[e] = z4();
       if (kk < BK && k < kend && col < N) {
         if (OP == OP_GATHER) {  // packed [K = tap*cb][cs]
           if (col + 3 < N && (g.cs & 3) == 0) {
@@ -439,8 +463,8 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
             v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
           }
         } else if (OP == OP_SCATTER) {  // packed [tap][cs][cb]; class taps
-          const int tap = k / g.cs, c = k - tap * g.cs;
-          const int jy = tap / ntx, jx = tap - jy * ntx;
+          const int tap = P.f_cs.div(k), c = k - tap * g.cs;
+          const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
           const int kh = ry + g.s * jy, kw = rx + g.s * jx;
           const size_t rowo = ((size_t)(kh * g.kw + kw) * g.cs + c) * g.cb;
           if (col + 3 < N && (g.cb & 3) == 0) {
@@ -466,27 +490,27 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           v = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
         } else {  // WGRAD: B(k = small pixel, col = (tap, cb)) = T(big[gather(pix, tap)][cb])
           const int hw = g.hs * g.ws;
-          const int nimg = k / hw, rem = k - nimg * hw;
-          const int ys = rem / g.ws, xs = rem - ys * g.ws;
+          const int nimg = P.f_hws.div(k), rem = k - nimg * hw;
+          const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
           const int nreal = P.N;
           if (col >= nreal) {  // bias column (nreal % 4 == 0 when gbias is used)
             v = make_float4(col == nreal ? 1.f : 0.f, 0.f, 0.f, 0.f);
           } else if (b_vec) {
-            const int tap = col / g.cb, c0 = col - tap * g.cb;
-            const int kh = tap / g.kw, kw = tap - kh * g.kw;
+            const int tap = P.f_cb.div(col), c0 = col - tap * g.cb;
+            const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
             const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
             if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
               const size_t off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + c0;
               v = ld4(P.b.x + off);
-              if (b_bwd) ryb[e] = ld4(P.b.y + off);
-              bmask |= 1u << e;
+              if (b_bwd) S.ryb[e] = ld4(P.b.y + off);
+              S.bmask |= 1u << e;
             }
           } else {
             float tmp[4] = {0.f, 0.f, 0.f, 0.f};
             for (int j = 0; j < 4 && col + j < nreal; ++j) {
               const int cc = col + j;
-              const int tap = cc / g.cb, c = cc - tap * g.cb;
-              const int kh = tap / g.kw, kw = tap - kh * g.kw;
+              const int tap = P.f_cb.div(cc), c = cc - tap * g.cb;
+              const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
               const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
               if ((unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
                 const size_t off = P.b.nchw ? ((size_t)(nimg * g.cb + c) * g.hb + yb) * g.wb + xb
@@ -503,19 +527,19 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           }
         }
       }
-      rb[e] = v;
+      S.rb[e] = v;
     }
   };
 
-  auto storeB = [&](float* Bb) {
+  auto storeB = [&](Stage& S, float* Bb) {
 #pragma unroll
     for (int e = 0; e < BW; ++e) {
       const int idx = t + NT * e;
       const int nq = idx % NQ, kk = idx / NQ;
-      float4 v = rb[e];
-      if (OP == OP_WGRAD && b_vec && P.b.xf != CV_XF_NONE && (bmask & (1u << e))) {
+      float4 v = S.rb[e];
+      if (OP == OP_WGRAD && b_vec && P.b.xf != CV_XF_NONE && (S.bmask & (1u << e))) {
         const int col = n0 + 4 * nq;
-        v = xf_apply4(P.b, cb, col % g.cb, v, ryb[e]);
+        v = xf_apply4(P.b, cb, P.f_cb.mod(col), v, S.ryb[e]);
       }
       if (kk < BK) *reinterpret_cast<float4*>(Bb + kk * LDB + 4 * nq) = v;
     }
@@ -528,43 +552,57 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  fetchA(kbeg);
-  fetchB(kbeg);
-  storeA(As, kbeg);
-  storeB(Bs);
+  // CV_DEPTH-deep register ring: tile t is staged in slot t % D; at step t the loads of tile t+D-1
+  // are issued, tile t is multiplied from LDS, then tile t+1 (loaded D-2 steps earlier) is
+  // transformed and stored to the other LDS buffer -- so D-1 tiles of loads are in flight across
+  // every MFMA phase.
+  constexpr int D = CV_DEPTH;
+  Stage stg[D];
+  const int nt = (kend - kbeg + BK - 1) / BK;
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) {
+    if (d < nt) {
+      fetchA(stg[d], kbeg + d * BK);
+      fetchB(stg[d], kbeg + d * BK);
+    }
+  }
+  storeA(stg[0], As, kbeg);
+  storeB(stg[0], Bs);
   __syncthreads();
-  int cur = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    if (more) {
-      fetchA(k0 + BK);
-      fetchB(k0 + BK);
-    }
-    const float* Ab = As + cur * ABUF;
-    const float* Bb = Bs + cur * BBUF;
+  for (int tb = 0; tb < nt; tb += D) {
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      const int kr = kk + (lane >> 4);
-      float av[FM], bv[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = wm * TM + i * 16 + (lane & 15);
-        av[i] = ROWS ? Ab[((kk >> 2) * BM + m) * 4 + (lane >> 4)] : Ab[kr * LDA + m];
+    for (int d = 0; d < D; ++d) {
+      const int tt = tb + d;
+      if (tt >= nt) break;
+      if (tt + D - 1 < nt) {
+        fetchA(stg[(d + D - 1) % D], kbeg + (tt + D - 1) * BK);
+        fetchB(stg[(d + D - 1) % D], kbeg + (tt + D - 1) * BK);
       }
+      const float* Ab = As + (tt & 1) * ABUF;
+      const float* Bb = Bs + (tt & 1) * BBUF;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bv[j] = Bb[kr * LDB + wn * TN + j * 16 + (lane & 15)];
+      for (int kk = 0; kk < BK; kk += 4) {
+        const int kr = kk + (lane >> 4);
+        float av[FM], bv[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) {
+          const int m = wm * TM + i * 16 + (lane & 15);
+          av[i] = ROWS ? Ab[((kk >> 2) * BM + m) * 4 + (lane >> 4)] : Ab[kr * LDA + m];
+        }
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) bv[j] = Bb[kr * LDB + wn * TN + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+      if (tt + 1 < nt) {
+        storeA(stg[(d + 1) % D], As + ((tt + 1) & 1) * ABUF, kbeg + (tt + 1) * BK);
+        storeB(stg[(d + 1) % D], Bs + ((tt + 1) & 1) * BBUF);
+      }
+      __syncthreads();
     }
-    if (more) {
-      storeA(As + (cur ^ 1) * ABUF, k0 + BK);
-      storeB(Bs + (cur ^ 1) * BBUF);
-    }
-    __syncthreads();
-    cur ^= 1;
   }
 
   // ---------------- epilogue
@@ -588,7 +626,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
             P.part[((size_t)bz * M + row) * N + col] = v;
             continue;
           }
-          const int tap = col / g.cb, c = col - tap * g.cb;  // w layout [cs][cb][kh][kw]
+          const int tap = P.f_cb.div(col), c = col - tap * g.cb;  // w layout [cs][cb][kh][kw]
           float* dst = (col >= P.N) ? P.gbias + row : P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap;
           if (gridDim.z == 1) *dst += v;  // single writer
           else atomicAdd(dst, v);
@@ -599,12 +637,12 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           off = (size_t)row * g.cs + col;
         } else if (OP == OP_SCATTER) {
           const int hw = cy * cx;
-          const int nimg = row / hw, rem = row - nimg * hw;
-          const int ty = rem / cx, tx = rem - ty * cx;
+          const int nimg = f_cycx.div(row), rem = row - nimg * hw;
+          const int ty = f_cx.div(rem), tx = rem - ty * cx;
           const int yb = yb0 + g.s * ty, xb = xb0 + g.s * tx;
           off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + col;
         } else {
-          const int oc = (P.o_pix > 1) ? (col % P.o_pix) * P.o_ch + col / P.o_pix : col;
+          const int oc = (P.o_pix > 1) ? P.f_opix.mod(col) * P.o_ch + P.f_opix.div(col) : col;
           off = (size_t)row * P.ldo + oc;
         }
         if (P.bias && (!P.accumulate || bz == 0)) v += P.bias[col];
@@ -613,7 +651,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           continue;
         }
         if (P.ep.stat_mode == CV_STAT_BWD) {
-          const int f = col / P.ep.stat_div;
+          const int f = P.f_sdiv.div(col);
           const float yv = P.ep.ey[off];
           const BnFwdC k = reinterpret_cast<const BnFwdC*>(cstE)[f];
           if (P.ep.erelu && bn_out(yv, k) <= 0.f) v = 0.f;
@@ -658,7 +696,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
           a += (double)red[w * BN + t];
           b += (double)red[WM * BN + w * BN + t];
         }
-        const int f = col / P.ep.stat_div;
+        const int f = P.f_sdiv.div(col);
         const int C = (P.ep.stat_mode == CV_STAT_BWD) ? P.ce_n : P.ep.ebn.C;
         const int repl = hw_id % CV_STAT_REPL(C);
         double* so = P.ep.stat_out + (size_t)repl * 2 * C;
@@ -742,7 +780,8 @@ static size_t lds_bytes(const Args& a, int BM_, int BN_) {
   const int WN = (BN_ >= 32) ? 2 : 1, WM = 4 / WN;
   const int LDA = (a.op == OP_WGRAD) ? BM_ + 16 : BM_, LDB = BN_ + ((BN_ % 32) == 0 ? 16 : 0);
   size_t f = 2 * ((size_t)BK * LDA + (size_t)BK * LDB) + 2 * WM * BN_;
-  f += xf_floats(a.a.xf, a.ca_n) + xf_floats(a.b.xf, a.cb_n);
+  const bool bn1d = a.op == OP_DENSE && a.ca_n == a.K && a.a.xf != CV_XF_NONE;
+  f += xf_floats(a.a.xf, bn1d ? a.kchunk : a.ca_n) + xf_floats(a.b.xf, a.cb_n);
   if (a.ep.stat_mode == CV_STAT_BWD) f += 4 * (size_t)a.ce_n;
   return f * sizeof(float);
 }
@@ -752,11 +791,12 @@ static int launch_t(const Args& a, dim3 grid, hipStream_t st) {
   const size_t lds = lds_bytes(a, BM, BN);
   CV_REQUIRE(lds <= 160 * 1024, "igemm: LDS request %zu bytes exceeds 160 KiB", lds);
   if (lds > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)igemm_kernel<OP, BM, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      attr_set = true;
+    const hipError_t e = hipFuncSetAttribute((const void*)igemm_kernel<OP, BM, BN>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      cv::set_error("igemm: LDS carve-out of %zu bytes refused: %s", lds, hipGetErrorString(e));
+      return 1;
     }
   }
   hipLaunchKernelGGL((igemm_kernel<OP, BM, BN>), grid, dim3(NT), lds, st, a);
@@ -776,7 +816,20 @@ static int launch_op(const Args& a, int BM_, int BN_, dim3 grid, hipStream_t st)
   return 1;
 }
 
+static void finalize_divs(Args& a) {
+  a.f_cb = FDiv::make(a.g.cb);
+  a.f_cs = FDiv::make(a.g.cs);
+  a.f_kw = FDiv::make(a.g.kw);
+  a.f_ws = FDiv::make(a.g.ws);
+  a.f_hws = FDiv::make((uint32_t)a.g.hs * a.g.ws);
+  a.f_ach = FDiv::make(a.a_ch);
+  a.f_opix = FDiv::make(a.o_pix);
+  a.f_sdiv = FDiv::make(a.ep.stat_div);
+  a.f_s = FDiv::make(a.g.s);
+}
+
 static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
+  finalize_divs(a);
   const int Ntot = a.N + ((a.op == OP_WGRAD && a.gbias) ? 1 : 0);
   const int gx = cdiv(a.M, BM_), gy = cdiv(Ntot, BN_);
   dim3 grid(gx, gy, gz);
@@ -971,6 +1024,18 @@ static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
   return w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
 }
 
+static int launch_wgrad_reduce(const float* part, int split, int M, int N, int ntot, int cb, int kk, float* gw,
+                               float* gbias, hipStream_t st) {
+  const int gx = cdiv((long)M * ntot, 64);
+  int gy = cdiv(split, 32);  // <= 32 slabs per block (8 per thread)
+  const int zper = cdiv(split, gy);
+  gy = cdiv(split, zper);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, part, split, zper, M, N, ntot, cb, kk, gw,
+                     gbias);
+  CV_LAUNCH_CHECK("wgrad_reduce");
+  return 0;
+}
+
 static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias,
                      int split_k, float* work, size_t work_bytes, hipStream_t st) {
   Args a;
@@ -999,15 +1064,7 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
     a.part = work;
   }
   if (launch(a, w.BM, w.BN, w.split, st)) return 1;
-  if (a.part) {
-    const int gx = cdiv((long)a.M * Ntot, 64);
-    int gy = cdiv(w.split, 32);  // <= 32 slabs per block (8 per thread)
-    const int zper = cdiv(w.split, gy);
-    gy = cdiv(w.split, zper);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, work, w.split, zper, a.M, a.N, Ntot,
-                       g.cb, g.kh * g.kw, gw, gbias);
-    CV_LAUNCH_CHECK("wgrad_reduce");
-  }
+  if (a.part) return launch_wgrad_reduce(work, w.split, a.M, a.N, Ntot, g.cb, g.kh * g.kw, gw, gbias, st);
   return 0;
 }
 

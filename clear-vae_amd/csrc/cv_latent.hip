@@ -11,14 +11,14 @@ namespace cv {
 
 // ---------------------------------------------------------------- reparameterisation
 // One workgroup; offset[0] is read by every thread and advanced by thread 0 after a barrier.
-__global__ __launch_bounds__(1024) void reparam_kernel(const float* __restrict__ heads, int n, int d,
+__global__ __launch_bounds__(256) void reparam_kernel(const float* __restrict__ heads, int n, int d,
                                                        const float* __restrict__ eps_in, uint64_t seed,
                                                        uint64_t* offset, float* __restrict__ z,
                                                        float* __restrict__ eps_out) {
   const uint64_t off = offset ? offset[0] : 0;
   const int zd = 2 * d;
   const long total = (long)n * zd;
-  for (long p = threadIdx.x; 2 * p < total; p += blockDim.x) {
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; 2 * p < total; p += (long)gridDim.x * blockDim.x) {
     float e2[2];
     if (!eps_in) normal2(seed, off, (uint64_t)p, e2[0], e2[1]);
 #pragma unroll
@@ -36,9 +36,9 @@ __global__ __launch_bounds__(1024) void reparam_kernel(const float* __restrict__
       if (eps_out) eps_out[e] = ep;
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && offset) offset[0] = off + 1;
 }
+
+__global__ void offset_advance_kernel(uint64_t* offset) { offset[0] += 1; }
 
 // single factor (module path): z = mu + eps*exp(lv/2); grid-stride, offset advanced by the last block
 __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
@@ -136,7 +136,11 @@ __global__ __launch_bounds__(1024) void combine_kernel(const float* __restrict__
   const double kc = block_sum<1024>(sc, scratch);
   const double ks = block_sum<1024>(ss, scratch);
   if (threadIdx.x == 0) {
-    if (rec_in) losses[0] = (float)rec_in[0];
+    if (rec_in) {
+      double r = 0.0;
+      for (int q = 0; q < CV_REC_REPL; ++q) r += rec_in[q];
+      losses[0] = (float)r;
+    }
     losses[1] = (float)(-0.5 * kc / (double)n);
     losses[2] = (float)(-0.5 * ks / (double)n);
     losses[7] = w;
@@ -488,8 +492,16 @@ extern "C" int cv_reparam_forward(const float* heads, int n, int d, const float*
   clear_error();
   CV_REQUIRE(heads && z && n > 0 && d > 0, "reparam_forward: bad args");
   CV_REQUIRE(eps || offset, "reparam_forward: need injected eps or a device offset counter");
-  hipLaunchKernelGGL(reparam_kernel, dim3(1), dim3(1024), 0, S(stream), heads, n, d, eps, seed, offset, z, eps_out);
+  long blocks = ((long)n * d + 255) / 256;  // one thread per pair of latents
+  if (blocks > 64) blocks = 64;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(reparam_kernel, dim3((int)blocks), dim3(256), 0, S(stream), heads, n, d, eps, seed, offset, z,
+                     eps_out);
   CV_LAUNCH_CHECK("reparam_forward");
+  if (offset) {  // the Philox offset moves once per call, after every block has read it
+    hipLaunchKernelGGL(offset_advance_kernel, dim3(1), dim3(1), 0, S(stream), offset);
+    CV_LAUNCH_CHECK("reparam_offset");
+  }
   return 0;
 }
 

@@ -461,42 +461,65 @@ __global__ __launch_bounds__(LN_T) void mi_learn_kernel(const LearnArgs A) {
 }
 
 // ---------------------------------------------------------------- Adam over a flat arena
+// torch.optim.Adam (foreach) over a flat arena: grid-stride float4 (the arena is 16-byte aligned and
+// padded to a multiple of 4), bias corrections computed once per block.  The step counters are
+// advanced by adam_advance_kernel right after (a one-thread launch, so no block has to detect being
+// the last one through a contended atomic).
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ gr,
                                                    float* __restrict__ m, float* __restrict__ v, long numel,
-                                                   const float* hyper, int64_t* step, const float* gscale,
-                                                   int64_t* aux) {
-  const long t_step = step[0] + 1;
-  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
-  const double bc1 = 1.0 - pow((double)b1, (double)t_step);
-  const double bc2 = 1.0 - pow((double)b2, (double)t_step);
-  const float step_size = (float)(-(double)lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
-  const float omb1 = (float)(1.0 - (double)b1), omb2 = (float)(1.0 - (double)b2);
-  const float gs = gscale ? gscale[0] : 1.0f;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < numel; i += (long)gridDim.x * 256) {
-    float g = gr[i];
-    if (gscale) g *= gs;
-    const float pp = p[i];
+                                                   const float* hyper, const int64_t* step, const float* gscale) {
+  __shared__ float cst[8];
+  if (threadIdx.x == 0) {
+    const long t_step = step[0] + 1;
+    const double b1 = hyper[1], b2 = hyper[2];
+    const double bc1 = 1.0 - pow(b1, (double)t_step);
+    const double bc2 = 1.0 - pow(b2, (double)t_step);
+    cst[0] = (float)(-(double)hyper[0] / bc1);
+    cst[1] = (float)sqrt(bc2);
+    cst[2] = (float)(1.0 - b1);
+    cst[3] = (float)(1.0 - b2);
+    cst[4] = hyper[2];
+    cst[5] = hyper[3];
+    cst[6] = hyper[4];
+    cst[7] = gscale ? gscale[0] : 1.0f;
+  }
+  __syncthreads();
+  const float step_size = cst[0], bc2s = cst[1], omb1 = cst[2], omb2 = cst[3], b2f = cst[4], eps = cst[5];
+  const float wd = cst[6], gs = cst[7];
+  const long n4 = numel >> 2;
+  auto upd = [&](float g, float pp, float& mm, float& vv) -> float {
+    g *= gs;
     if (wd != 0.f) g = g + wd * pp;
-    float mm = m[i];
     mm = mm + omb1 * (g - mm);
-    float vv = v[i] * b2;
-    vv = vv + omb2 * g * g;
+    vv = vv * b2f + omb2 * g * g;
+    const float den = sqrtf(vv) / bc2s + eps;
+    return pp + step_size * (mm / den);
+  };
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 g4 = reinterpret_cast<const float4*>(gr)[i];
+    float4 p4 = reinterpret_cast<float4*>(p)[i];
+    float4 m4 = reinterpret_cast<float4*>(m)[i];
+    float4 v4 = reinterpret_cast<float4*>(v)[i];
+    p4.x = upd(g4.x, p4.x, m4.x, v4.x);
+    p4.y = upd(g4.y, p4.y, m4.y, v4.y);
+    p4.z = upd(g4.z, p4.z, m4.z, v4.z);
+    p4.w = upd(g4.w, p4.w, m4.w, v4.w);
+    reinterpret_cast<float4*>(m)[i] = m4;
+    reinterpret_cast<float4*>(v)[i] = v4;
+    reinterpret_cast<float4*>(p)[i] = p4;
+  }
+  for (long i = (n4 << 2) + (long)blockIdx.x * 256 + threadIdx.x; i < numel; i += (long)gridDim.x * 256) {
+    float mm = m[i], vv = v[i];
+    p[i] = upd(gr[i], p[i], mm, vv);
     m[i] = mm;
     v[i] = vv;
-    const float den = sqrtf(vv) / bc2s + eps;
-    p[i] = pp + step_size * (mm / den);
   }
-  // last workgroup advances the step counters (step[1] is the arrival counter)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long prev = atomicAdd((unsigned long long*)(step + 1), 1ull);
-    if (prev == (unsigned long long)(gridDim.x - 1)) {
-      step[0] = t_step;
-      step[1] = 0;
-      if (aux) aux[0] += 1;
-    }
-  }
+}
+
+__global__ void adam_advance_kernel(int64_t* step, int64_t* aux) {
+  step[0] += 1;
+  step[1] = 0;
+  if (aux) aux[0] += 1;
 }
 
 }  // namespace cv
@@ -587,10 +610,15 @@ extern "C" int cv_adam_step(float* params, const float* grads, float* exp_avg, f
                             cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(params && grads && exp_avg && exp_avg_sq && hyper && step && numel > 0, "adam_step: bad args");
-  long g = (numel + 255) / 256;
-  if (g > 1024) g = 1024;
+  CV_REQUIRE(((uintptr_t)params | (uintptr_t)grads | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+             "adam_step: buffers must be 16-byte aligned");
+  long g = (numel / 4 + 255) / 256;
+  if (g > 512) g = 512;
+  if (g < 1) g = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(g), dim3(256), 0, S(stream), params, grads, exp_avg, exp_avg_sq, (long)numel,
-                     hyper, step, grad_scale, aux_counter);
+                     hyper, step, grad_scale);
   CV_LAUNCH_CHECK("adam_step");
+  hipLaunchKernelGGL(adam_advance_kernel, dim3(1), dim3(1), 0, S(stream), step, aux_counter);
+  CV_LAUNCH_CHECK("adam_advance");
   return 0;
 }

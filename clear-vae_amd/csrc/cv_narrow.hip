@@ -95,6 +95,9 @@ __global__ __launch_bounds__(NNT) void narrow_gather_kernel(const NArgs P) {
   __syncthreads();
 
   const int q = t % NQ, pl = t / NQ;
+  float4 wq[K];  // this lane's channel quad of every tap's weights (K <= 16)
+#pragma unroll
+  for (int i = 0; i < K; ++i) wq[i] = Ws[i * NQ + q];
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   const int hw = g.hs * g.ws;
   for (long p = (long)blockIdx.x * PPB + pl; p < P.M; p += (long)gridDim.x * PPB) {
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(NNT) void narrow_gather_kernel(const NArgs P) {
       const bool ok = (okm >> i) & 1ull;
       if (xf == CV_XF_BNRELU) a = ok ? bn_relu(a, kf[c]) : 0.f;
       else if (xf == CV_XF_BNBWD) a = ok ? bn_bwd(a, yv[i], kb[c]) : 0.f;
-      const float4 w4 = Ws[i * NQ + q];
+      const float4 w4 = wq[i];
       acc.x = fmaf(a, w4.x, acc.x);
       acc.y = fmaf(a, w4.y, acc.y);
       acc.z = fmaf(a, w4.z, acc.z);
@@ -229,6 +232,33 @@ __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
   const int ntx = (g.kw > rx) ? (g.kw - rx + s - 1) / s : 0;
   const long Mc = (long)g.n * cy * cx;
   const int sub = t % LPP, c0 = sub * CPL;
+  // this lane's 8 channels: BatchNorm constants and the class's tap weights live in registers
+  float k_sc[CPL], k_mu[CPL], k_be[CPL], k_c1[CPL], k_c2[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) {
+    k_sc[e] = 1.f; k_mu[e] = 0.f; k_be[e] = 0.f; k_c1[e] = 0.f; k_c2[e] = 0.f;
+    if (xf == CV_XF_BNRELU) {
+      const BnFwdC k = kf[c0 + e];
+      k_sc[e] = k.sc; k_mu[e] = k.mu; k_be[e] = k.be;
+    } else if (xf == CV_XF_BNBWD) {
+      const BnBwdC k = kb[c0 + e];
+      k_sc[e] = k.sc; k_mu[e] = k.mu; k_be[e] = k.istd; k_c1[e] = k.c1; k_c2[e] = k.c2;
+    }
+  }
+  float wr[TP][CPL][CB];
+#pragma unroll
+  for (int jy = 0; jy < NT2; ++jy)
+#pragma unroll
+    for (int jx = 0; jx < NT2; ++jx) {
+      const int kh = ry + s * jy, kw = rx + s * jx;
+      const bool tap_ok = jy < nty && jx < ntx;
+#pragma unroll
+      for (int e = 0; e < CPL; ++e)
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+          wr[jy * NT2 + jx][e][j] = tap_ok ? Wl[((kh * g.kw + kw) * CS + c0 + e) * CB + j] : 0.f;
+    }
+  const FDiv f_cycx = FDiv::make(cy * cx), f_cx = FDiv::make(cx);
   float s1[CB], s2[CB];
 #pragma unroll
   for (int j = 0; j < CB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
@@ -238,10 +268,10 @@ __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
   for (long it = 0; it < trips; ++it) {
     const long r = it * rstride + (long)blockIdx.x * (NNT / LPP) + t / LPP;
     const bool live = r < Mc;
-    const long rr = live ? r : 0;
-    const int n = (int)(rr / (cy * cx));
-    const int rem = (int)(rr - (long)n * cy * cx);
-    const int ty = rem / cx, tx = rem - ty * cx;
+    const int rr = live ? (int)r : 0;
+    const int n = f_cycx.div(rr);
+    const int rem = rr - n * cy * cx;
+    const int ty = f_cx.div(rem), tx = rem - ty * cx;
     const int yb = yb0 + s * ty, xb = xb0 + s * tx;
     float4 xv[TP][2], yv4[TP][2];
     bool ok[TP];
@@ -252,7 +282,7 @@ __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
         const int tp = jy * NT2 + jx;
         const int kh = ry + s * jy, kw = rx + s * jx;
         const int py = yb + g.p - kh, px = xb + g.p - kw;
-        const int ys = py / s, xs = px / s;
+        const int ys = py >> 1, xs = px >> 1;  // s == 2 (host-checked); exact within the class
         ok[tp] = live && jy < nty && jx < ntx && py >= 0 && px >= 0 && ys < g.hs && xs < g.ws;
         xv[tp][0] = xv[tp][1] = make_float4(0.f, 0.f, 0.f, 0.f);
         yv4[tp][0] = yv4[tp][1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -276,8 +306,6 @@ __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
       for (int jx = 0; jx < NT2; ++jx) {
         const int tp = jy * NT2 + jx;
         if (!ok[tp]) continue;
-        const int kh = ry + s * jy, kw = rx + s * jx;
-        const float* wt = Wl + ((kh * g.kw + kw) * CS + c0) * CB;
         const float xs8[8] = {xv[tp][0].x, xv[tp][0].y, xv[tp][0].z, xv[tp][0].w,
                               xv[tp][1].x, xv[tp][1].y, xv[tp][1].z, xv[tp][1].w};
         const float ys8[8] = {yv4[tp][0].x, yv4[tp][0].y, yv4[tp][0].z, yv4[tp][0].w,
@@ -285,10 +313,10 @@ __global__ __launch_bounds__(NNT) void narrow_scatter_kernel(const NArgs P) {
 #pragma unroll
         for (int e = 0; e < CPL; ++e) {
           float a = xs8[e];
-          if (xf == CV_XF_BNRELU) a = bn_relu(a, kf[c0 + e]);
-          else if (xf == CV_XF_BNBWD) a = bn_bwd(a, ys8[e], kb[c0 + e]);
+          if (xf == CV_XF_BNRELU) a = fmaxf(fmaf(a - k_mu[e], k_sc[e], k_be[e]), 0.f);
+          else if (xf == CV_XF_BNBWD) a = k_sc[e] * (a - k_c1[e] - (ys8[e] - k_mu[e]) * k_be[e] * k_c2[e]);
 #pragma unroll
-          for (int j = 0; j < CB; ++j) acc[j] = fmaf(a, wt[e * CB + j], acc[j]);
+          for (int j = 0; j < CB; ++j) acc[j] = fmaf(a, wr[tp][e][j], acc[j]);
         }
       }
 #pragma unroll
@@ -336,7 +364,7 @@ static int grid_for(long M) {
 int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const float* bias, float* out,
                   const cv_epilogue* ep, hipStream_t st) {
   if (g.cs != 32 || g.kh != g.kw || (g.kh != 3 && g.kh != 4) || (g.cb != 1 && g.cb != 3)) return -1;
-  if (g.kh * g.kw * g.cb > 16) return -1;  // K = 48 (3-channel 4x4) is a real contraction: MFMA igemm
+  if (g.cb != 1) return -1;  // K = 27 / 48 (3-channel images) is a real contraction: MFMA igemm
   if (in->xf != CV_XF_NONE) CV_REQUIRE(in->bn.C == g.cb, "narrow_gather: BN width %d != %d", in->bn.C, g.cb);
   if (check_ep(ep, g.cs, "narrow_gather")) return 1;
   NArgs a;
@@ -352,10 +380,8 @@ int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const flo
   long blocks = (a.M + 31) / 32;  // 32 pixels per block iteration
   if (blocks > 1024) blocks = 1024;
   const dim3 grid((int)blocks), blk(NNT);
-  if (g.kh == 3 && g.cb == 1) hipLaunchKernelGGL((narrow_gather_kernel<32, 3, 1>), grid, blk, 0, st, a);
-  else if (g.kh == 3) hipLaunchKernelGGL((narrow_gather_kernel<32, 3, 3>), grid, blk, 0, st, a);
-  else if (g.cb == 1) hipLaunchKernelGGL((narrow_gather_kernel<32, 4, 1>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((narrow_gather_kernel<32, 4, 3>), grid, blk, 0, st, a);
+  if (g.kh == 3) hipLaunchKernelGGL((narrow_gather_kernel<32, 3, 1>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((narrow_gather_kernel<32, 4, 1>), grid, blk, 0, st, a);
   CV_LAUNCH_CHECK("narrow_gather");
   return 0;
 }

@@ -17,7 +17,11 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int64, c_size_t, c_uint6
 import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libclearvae_hip.so")
+# CVHIP_LIB overrides the in-tree library (kernel-variant experiments only)
+LIB_PATH = os.environ.get("CVHIP_LIB") or os.path.join(_HERE, "libclearvae_hip.so")
+
+REC_REPL = 32  # CV_REC_REPL
+
 
 def stat_repl(C: int) -> int:
     """CV_STAT_REPL(C) of include/clearvae.h: replicas of a C-feature fp64 statistics buffer."""

@@ -261,7 +261,7 @@ class ClearStep:
         lat = Program()
         lat.add("cv_latent_combine", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
                 ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
-                ws.scal[0:1], ws.dheads, ws.losses)
+                ws.rec, ws.dheads, ws.losses)
         hb = ws.heads.data_ptr()
         dh = ws.dheads.data_ptr()
         alpha = float(hp["alpha"])

@@ -394,7 +394,7 @@ class Workspace:
         # fp64 statistics arena: per BN layer [REPL,2,C] forward + [REPL,2,C] backward, plus scalars
         bns = spec.bn_layers
         counts = [n * c.h_out * c.w_out for c in spec.enc] + [n] + [n * c.h_out * c.w_out for c in spec.dec]
-        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 16
+        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 64
         self.stats = torch.zeros(tot, dtype=torch.float64, device=device)
         self.bnv = []
         o = 0
@@ -405,7 +405,8 @@ class Workspace:
             gs = self.stats[o + sz:o + 2 * sz].view(R, 2, b.num_features)
             self.bnv.append(BNView(b, st, gs, cnt))
             o += 2 * sz
-        self.scal = self.stats[o:o + 16]  # [0] rec sum, [1] mse work
+        self.scal = self.stats[o:o + 64]  # [0:REC_REPL] rec replicas (cv_output_loss), [32] mse work
+        self.rec = self.scal[0:_lib.REC_REPL]
         self.bn_enc = self.bnv[: len(spec.enc)]
         self.bn_1d = self.bnv[len(spec.enc)]
         self.bn_dec = self.bnv[len(spec.enc) + 1:]
@@ -492,7 +493,7 @@ class Workspace:
         elif output == "loss":
             assert train
             P.add("cv_output_loss", self.bn_dec[-1].cv(True), cur, x, n, sp.in_ch, hw, self.xhat,
-                  self.scal[0:1], self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
+                  self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
 
     def decoder_backward_program(self, P: Program, param_grad, dz_out):
         """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to

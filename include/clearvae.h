@@ -32,6 +32,7 @@ typedef void* cv_stream_t; /* a hipStream_t (torch.cuda.current_stream().cuda_st
 
 /* Replicas of a C-feature statistics buffer: narrow layers get more replicas so that the fp64
  * atomics of thousands of producer workgroups do not serialise on a few addresses. */
+#define CV_REC_REPL 32
 #define CV_STAT_REPL(C) ((C) >= 256 ? 8 : (C) >= 64 ? 16 : 32)
 
 /* ---- BatchNorm as seen by a fused prologue/epilogue (nn.BatchNorm1d/2d, vae.py:17-44, 115-154) ---- */
@@ -163,8 +164,9 @@ int cv_bn_batch_stats(const cv_bn* bn, float* mean, float* invstd, cv_stream_t s
 /* xhat = sigmoid(BN(y)), written NCHW [n][c][h][w]; y is NHWC [n][h][w][c]. */
 int cv_output_forward(const cv_bn* bn, const float* y, int n, int c, int hw, float* xhat,
                       cv_stream_t stream);
-/* fused output + reconstruction loss (losses.py:36-47): rec = mean_n sum_chw (xhat - x)^2 into
- * rec_out[0] (fp64 accumulate; caller zeroes), and when dv_out != NULL the gradient of
+/* fused output + reconstruction loss (losses.py:36-47): rec = mean_n sum_chw (xhat - x)^2,
+ * accumulated into the CV_REC_REPL fp64 replicas rec_out[0..CV_REC_REPL) (caller zeroes; rec is
+ * their sum), and when dv_out != NULL the gradient of
  * (rec_scale*rec) w.r.t. the BN output: dv = rec_scale*2(xhat-x)/n * xhat(1-xhat) (NHWC), plus the
  * BN backward sums into gstat_out.  rec_scale may be NULL (1.0). x is NCHW. */
 int cv_output_loss(const cv_bn* bn, const float* y, const float* x, int n, int c, int hw,
@@ -202,7 +204,8 @@ int cv_kl(const float* mu, const float* logvar, int ld, int n, int d, float* kl_
 
 /* Fused-step seed of d(heads): KL(c), KL(s) with the LogisticAnnealer weight
  * w = beta/(1+exp(-(t-loc)/scale)), t = anneal_step[0] (trainer.py:22-38, 474-477), plus the decoder
- * gradient dz chained through z = mu + eps*exp(lv/2).  losses[0] = rec_in[0] (if given),
+ * gradient dz chained through z = mu + eps*exp(lv/2).  losses[0] = sum of the CV_REC_REPL
+ * replicas rec_in[] of cv_output_loss (if given),
  * losses[1], losses[2] = kl_c, kl_s; losses[7] = w.  dheads is overwritten. */
 int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                       float loc, float scale, const int64_t* anneal_step, const double* rec_in,
