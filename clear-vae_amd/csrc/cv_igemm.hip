@@ -844,8 +844,6 @@ static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
 }
 
 // Row-oriented tile: prefer 64-wide N tiles, shrink N (keeping BM=64) until there are >= 512
-// workgroups to cover the 256 CUs twice; BM=128 only for very tall problems.
-// Row-oriented tile: prefer 64-wide N tiles, shrink N (keeping BM=64) until there are >= 512
 // workgroups; BM=128 only for very tall problems.  (Measured against BM=128-first and >=256/384/768/
 // 1024-workgroup variants on both bench configs: this one is best or within noise.)
 static void pick_tile(long M, int N, int& BM_, int& BN_) {
