@@ -1,0 +1,686 @@
+// Specialised implicit-GEMM core on fp32 MFMA (v_mfma_f32_16x16x4_f32) for gfx950.
+//
+// Serves the same four contractions as cv_igemm.hip (GATHER / SCATTER / WGRAD / DENSE, see there),
+// restricted to vectorisable operands (channel counts that are multiples of 4, NHWC), which is every
+// conv / linear layer of VAE and VAE64 except the image-facing ones.  What differs from the generic
+// kernel, and why (per-block timeline stamps of the generic kernel: ~1.6 us per K tile = ~3,600
+// cycles for 16 MFMAs per wave, and a 4-13 us prologue):
+//   * the operand transforms (BN+ReLU forward, BN backward) and the epilogue statistics mode are
+//     template parameters, so the staging code has no per-element branches;
+//   * both LDS operand images are k-contiguous, [row][BK + 4]: a lane's ds_read_b128 returns the
+//     4 consecutive k of its row, which feed 4 successive MFMAs (step s of a 16-k chunk uses
+//     k = 4*(lane/16) + s for lane group lane/16 on both operands, so the contraction is unchanged).
+//     One b128 read per 4 MFMAs instead of one b32 read per MFMA; the row pitch of 36 floats makes
+//     the 16 rows of a fragment read land on 16 disjoint 4-bank groups (conflict free);
+//   * every global load of a K tile is issued unconditionally (out-of-range lanes read element 0
+//     and are zeroed by a select afterwards; the tail tiles re-read the last tile), so the number of
+//     loads in flight is static and the compiler's vmcnt waits let D-1 tiles stay in flight across
+//     the MFMA phases (a register ring of D stages; D=2 is the classic double buffer);
+//   * the BatchNorm constants are folded from the fp64 replica sums into SoA LDS arrays (float4
+//     reads at store time) AFTER the first tiles' loads are issued, so the fold's latency hides
+//     under them.
+#pragma once
+#include "cv_igemm.hpp"
+
+namespace cv {
+namespace fast {
+
+constexpr int LDK = BK + 4;  // LDS row pitch (floats) of both k-contiguous operand images
+
+__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 g4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// SoA constants: BNRELU [sc][mu][be], BNBWD [sc][c1][mu][istd][c2], each nf floats
+template <int XF>
+__host__ __device__ constexpr int soa_arrays() {
+  return XF == CV_XF_BNRELU ? 3 : XF == CV_XF_BNBWD ? 5 : 0;
+}
+
+// same arithmetic, in the same order, as bn_relu / bn_bwd of cv_common.hpp
+template <int XF>
+__device__ __forceinline__ f32x4 xform4(f32x4 x, f32x4 y, const float* c, int nf, int ch) {
+  if constexpr (XF == CV_XF_BNRELU) {
+    const f32x4 sc = lds4(c + ch), mu = lds4(c + nf + ch), be = lds4(c + 2 * nf + ch);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = fmaxf(fmaf(x[j] - mu[j], sc[j], be[j]), 0.f);
+  } else if constexpr (XF == CV_XF_BNBWD) {
+    const f32x4 sc = lds4(c + ch), c1 = lds4(c + nf + ch), mu = lds4(c + 2 * nf + ch);
+    const f32x4 is = lds4(c + 3 * nf + ch), c2 = lds4(c + 4 * nf + ch);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = sc[j] * (x[j] - c1[j] - (y[j] - mu[j]) * is[j] * c2[j]);
+  }
+  return x;
+}
+
+template <int XF>
+__device__ __forceinline__ void fill_soa(const cv_bn& bn, int nf, float* dst, double* scratch) {
+  if constexpr (XF == CV_XF_BNRELU) {
+    bn_fold<NT>(bn, false, scratch, [&](int f, double s, double q, double, double) {
+      if (f < nf) {
+        const BnFwdC k = bn_fwd_const_s(bn, f, s, q);
+        dst[f] = k.sc;
+        dst[nf + f] = k.mu;
+        dst[2 * nf + f] = k.be;
+      }
+    });
+  } else if constexpr (XF == CV_XF_BNBWD) {
+    bn_fold<NT>(bn, true, scratch, [&](int f, double s, double q, double gs, double gq) {
+      if (f < nf) {
+        const BnBwdC k = bn_bwd_const_s(bn, f, s, q, gs, gq);
+        dst[f] = k.sc;
+        dst[nf + f] = k.c1;
+        dst[2 * nf + f] = k.mu;
+        dst[3 * nf + f] = k.istd;
+        dst[4 * nf + f] = k.c2;
+      }
+    });
+  }
+}
+
+// DENSE B modes (the XB slot of a DENSE instance)
+enum { DB_KCONT = 0, DB_NCONT = 1, DB_KPERM = 2 };
+
+template <int OP, int BM, int BN>
+struct Shape {
+  static constexpr int WN = (BN >= 32) ? 2 : 1;
+  static constexpr int WM = 4 / WN;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int RA = BM / 32;                  // A float4 slots per thread (BM*BK/4/NT)
+  static constexpr int RB = (BN * BK / 4 + NT - 1) / NT;  // B float4 slots per thread
+};
+
+// LDS floats: 2 A images + 2 B images + epilogue reduction + constants
+__host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int nfb, int nfe) {
+  const int WN = (BN >= 32) ? 2 : 1, WM = 4 / WN;
+  return 2 * (size_t)BM * LDK + 2 * (size_t)BN * LDK + 2 * WM * BN + nfa + nfb + nfe;
+}
+
+template <int OP, int BM, int BN, int XA, int XB, int EPI, int D>
+__global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
+  using SH = Shape<OP, BM, BN>;
+  constexpr int WN = SH::WN, WM = SH::WM, TM = SH::TM, TN = SH::TN, FM = SH::FM, FN = SH::FN;
+  constexpr int RA = SH::RA, RB = SH::RB;
+  static_assert(FM >= 1 && FN >= 1 && RA >= 1, "tile too small");
+  constexpr bool ROWS = OP != OP_WGRAD;
+  constexpr int XFB = (OP == OP_WGRAD) ? XB : CV_XF_NONE;  // B transform (WGRAD only)
+  constexpr bool AY = XA == CV_XF_BNBWD, BYY = XFB == CV_XF_BNBWD;
+  constexpr int DBM = (OP == OP_DENSE) ? XB : DB_NCONT;    // B staging mode
+  constexpr bool BKC = (DBM == DB_KCONT || DBM == DB_KPERM);
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                       // [2][BM][LDK]
+  float* Bs = As + 2 * BM * LDK;          // [2][BN][LDK]
+  float* red = Bs + 2 * BN * LDK;         // [2][WM][BN]
+  const bool bn1d = (OP == OP_DENSE) && XA != CV_XF_NONE && P.ca_n == P.K;
+  const int nfa = (XA == CV_XF_NONE) ? 0 : (bn1d ? P.kchunk : P.ca_n);
+  const int nfb = (XFB == CV_XF_NONE) ? 0 : P.cb_n;
+  float* cA = red + 2 * WM * BN;
+  float* cB = cA + soa_arrays<XA>() * nfa;
+  float* cE = cB + soa_arrays<XFB>() * nfb;  // STAT_BWD: BnFwdC of the epilogue's BN layer
+
+  CV_STAMP(st0);
+#ifdef CV_STAMPS
+  const unsigned long long mt0 = __builtin_amdgcn_s_memtime();
+#endif
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const Geo& g = P.g;
+
+  // ---------------- block -> (m0, n0, k-range, class): identical to the generic kernel
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int nwg = gx * gy * gridDim.z;
+  const int hw_id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (OP == OP_WGRAD) {
+    const int xcd = hw_id & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (hw_id >> 3);
+    by = lid % gy;
+    bx = (lid / gy) % gx;
+    bz = lid / (gx * gy);
+  }
+  const int m0 = bx * BM, n0 = by * BN;
+  int M = P.M, K = P.K;
+  const int N = P.N + ((OP == OP_WGRAD && P.gbias) ? 1 : 0);
+  int kbeg = 0, kend = K;
+  int ry = 0, rx = 0, yb0 = 0, xb0 = 0, cy = 1, cx = 1, ntx = 1;
+  FDiv f_cx = FDiv::make(1), f_cycx = FDiv::make(1), f_ntx = FDiv::make(1);
+  if (OP == OP_SCATTER) {
+    const int s = g.s, cls = bz;
+    ry = cls / s;
+    rx = cls % s;
+    yb0 = (((ry - g.p) % s) + s) % s;
+    xb0 = (((rx - g.p) % s) + s) % s;
+    cy = (g.hb > yb0) ? (g.hb - yb0 + s - 1) / s : 0;
+    cx = (g.wb > xb0) ? (g.wb - xb0 + s - 1) / s : 0;
+    const int nty = (g.kh > ry) ? (g.kh - ry + s - 1) / s : 0;
+    ntx = (g.kw > rx) ? (g.kw - rx + s - 1) / s : 0;
+    M = g.n * cy * cx;
+    K = nty * ntx * g.cs;
+    kend = K;
+    if (m0 >= M) return;
+    f_cx = FDiv::make(cx);
+    f_cycx = FDiv::make(cy * cx);
+    f_ntx = FDiv::make(ntx);
+  } else {
+    kbeg = bz * P.kchunk;
+    kend = min(K, kbeg + P.kchunk);
+    if (kbeg >= kend) return;
+  }
+  const int nt = (kend - kbeg + BK - 1) / BK;
+
+  // ---------------- per-thread A rows (row-oriented ops): rows (t>>3) + 32 i, k quad t & 7
+  const int aq = t & 7, ar = t >> 3;
+  int r_n[RA], r_y[RA], r_x[RA];
+  bool r_ok[RA];
+  if constexpr (ROWS) {
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const int r = m0 + ar + 32 * i;
+      r_ok[i] = r < M;
+      const int rr = r_ok[i] ? r : 0;
+      if (OP == OP_GATHER) {
+        const int hw = g.hs * g.ws;
+        r_n[i] = P.f_hws.div(rr);
+        const int rem = rr - r_n[i] * hw;
+        const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
+        r_y[i] = ys * g.s - g.p;
+        r_x[i] = xs * g.s - g.p;
+      } else if (OP == OP_SCATTER) {
+        const int hw = cy * cx;
+        r_n[i] = f_cycx.div(rr);
+        const int rem = rr - r_n[i] * hw;
+        const int ty = f_cx.div(rem), tx = rem - ty * cx;
+        r_y[i] = yb0 + g.s * ty + g.p;
+        r_x[i] = xb0 + g.s * tx + g.p;
+      } else {
+        r_n[i] = rr;
+        r_y[i] = 0;
+        r_x[i] = 0;
+      }
+    }
+  }
+
+  auto lf = [&](int kk) -> int {  // DENSE: PyTorch feature index of storage-order k'
+    if (P.a_pix <= 1) return kk;
+    const int pix = P.f_ach.div(kk), c = kk - pix * P.a_ch;
+    return c * P.a_pix + pix;
+  };
+
+  struct Stage {
+    f32x4 a[RA], ay[AY ? RA : 1];
+    f32x4 b[RB], by[BYY ? RB : 1];
+    unsigned am, bm, bone;  // validity masks; bone: WGRAD bias-column slots
+    int ach;                // channel index of the A transform constants
+  };
+
+  // ---------------- global -> registers (every load unconditional)
+  auto fetch = [&](Stage& S, int k0) {
+    S.am = 0;
+    S.bm = 0;
+    S.bone = 0;
+    const float* ax = P.a.x;
+    const float* ayp = P.a.y;
+    if constexpr (ROWS) {
+      const int kq = k0 + 4 * aq;
+      const bool kok = kq < kend;
+      if constexpr (OP == OP_GATHER) {
+        const int tap = P.f_cb.div(kq), c0 = kq - tap * g.cb;
+        const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
+        S.ach = c0;
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          const int yb = r_y[i] + kh, xb = r_x[i] + kw;
+          const bool ok = r_ok[i] && kok && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
+          int off = ((r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
+          off = ok ? off : 0;
+          S.a[i] = g4(ax + off);
+          if constexpr (AY) S.ay[i] = g4(ayp + off);
+          S.am |= (ok ? 1u : 0u) << i;
+        }
+      } else if constexpr (OP == OP_SCATTER) {
+        const int tap = P.f_cs.div(kq), c0 = kq - tap * g.cs;
+        const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
+        const int kh = ry + g.s * jy, kw = rx + g.s * jx;
+        S.ach = c0;
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          const int py = r_y[i] - kh, px = r_x[i] - kw;  // multiples of s by construction
+          const int ys = P.f_s.div(max(py, 0)), xs = P.f_s.div(max(px, 0));
+          const bool ok = r_ok[i] && kok && py >= 0 && px >= 0 && ys < g.hs && xs < g.ws;
+          int off = ((r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c0;
+          off = ok ? off : 0;
+          S.a[i] = g4(ax + off);
+          if constexpr (AY) S.ay[i] = g4(ayp + off);
+          S.am |= (ok ? 1u : 0u) << i;
+        }
+      } else {  // DENSE, storage-order k'
+        S.ach = bn1d ? kq - kbeg : (P.a_pix > 1 ? P.f_ach.mod(kq) : kq);
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          const bool ok = r_ok[i] && kok;
+          int off = r_n[i] * P.lda + kq;
+          off = ok ? off : 0;
+          S.a[i] = g4(ax + off);
+          if constexpr (AY) S.ay[i] = g4(ayp + off);
+          S.am |= (ok ? 1u : 0u) << i;
+        }
+      }
+    } else {  // WGRAD A(m = cs, k = small pixel): float4 along cs
+      constexpr int MQ = BM / 4;
+#pragma unroll
+      for (int e = 0; e < RA; ++e) {
+        const int idx = t + NT * e;
+        const int mq = idx % MQ, kk = idx / MQ;
+        const int pix = k0 + kk, c0 = m0 + 4 * mq;
+        const bool ok = pix < kend && c0 < g.cs;
+        int off = pix * g.cs + c0;
+        off = ok ? off : 0;
+        S.a[e] = g4(ax + off);
+        if constexpr (AY) S.ay[e] = g4(ayp + off);
+        S.am |= (ok ? 1u : 0u) << e;
+      }
+      S.ach = 0;
+    }
+
+    // B
+#pragma unroll
+    for (int e = 0; e < RB; ++e) {
+      const int idx = t + NT * e;
+      if constexpr (BKC) {  // DENSE layout 0: 4 consecutive k of one output column
+        const int n = idx >> 3, kq = k0 + 4 * (idx & 7), col = n0 + n;
+        const bool ok = n < BN && col < N && kq < kend;
+        if constexpr (DBM == DB_KCONT) {
+          int off = col * P.ldb + kq;
+          off = ok ? off : 0;
+          S.b[e] = g4(P.w + off);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int off = col * P.ldb + lf(kq + j);
+            off = ok ? off : 0;
+            S.b[e][j] = P.w[off];
+          }
+        }
+        S.bm |= (ok ? 1u : 0u) << e;
+      } else {
+        constexpr int NQ = BN / 4;
+        const int nq = idx % NQ, kk = idx / NQ;
+        const int col = n0 + 4 * nq, k = k0 + kk;
+        bool ok = kk < BK && k < kend && col < N;
+        int off = 0;
+        if constexpr (OP == OP_GATHER) {
+          off = k * g.cs + col;
+        } else if constexpr (OP == OP_SCATTER) {
+          const int tap = P.f_cs.div(k), c = k - tap * g.cs;
+          const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
+          const int kh = ry + g.s * jy, kw = rx + g.s * jx;
+          off = ((kh * g.kw + kw) * g.cs + c) * g.cb + col;
+        } else if constexpr (OP == OP_DENSE) {
+          off = lf(k) * P.ldb + col;
+        } else {  // WGRAD: B(k = small pixel, col = (tap, cb)) = T(big[gather(pix, tap)][cb])
+          const int hw = g.hs * g.ws;
+          const int nimg = P.f_hws.div(k), rem = k - nimg * hw;
+          const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
+          const int nreal = P.N;
+          const int tap = P.f_cb.div(col), c0 = col - tap * g.cb;
+          const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
+          const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
+          if (ok && col == nreal) S.bone |= 1u << e;
+          ok = ok && col < nreal && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
+          off = ((nimg * g.hb + yb) * g.wb + xb) * g.cb + c0;
+        }
+        off = ok ? off : 0;
+        const float* bx_ = (OP == OP_WGRAD) ? P.b.x : P.w;
+        S.b[e] = g4(bx_ + off);
+        if constexpr (BYY) S.by[e] = g4(P.b.y + off);
+        S.bm |= (ok ? 1u : 0u) << e;
+      }
+    }
+  };
+
+  // ---------------- transform + registers -> LDS
+  auto store = [&](Stage& S, int buf) {
+    float* Ab = As + buf * BM * LDK;
+    float* Bb = Bs + buf * BN * LDK;
+    if constexpr (ROWS) {
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        f32x4 v = S.a[i];
+        if constexpr (XA == CV_XF_BNRELU) v = xform4<XA>(v, v, cA, nfa, S.ach);
+        if constexpr (XA == CV_XF_BNBWD) v = xform4<XA>(v, S.ay[i], cA, nfa, S.ach);
+        if (!((S.am >> i) & 1u)) v = zero4();
+        *reinterpret_cast<f32x4*>(Ab + (ar + 32 * i) * LDK + 4 * aq) = v;
+      }
+    } else {
+      constexpr int MQ = BM / 4;
+#pragma unroll
+      for (int e = 0; e < RA; ++e) {
+        const int idx = t + NT * e;
+        const int mq = idx % MQ, kk = idx / MQ;
+        f32x4 v = S.a[e];
+        if constexpr (XA == CV_XF_BNRELU) v = xform4<XA>(v, v, cA, nfa, m0 + 4 * mq);
+        if constexpr (XA == CV_XF_BNBWD) v = xform4<XA>(v, S.ay[e], cA, nfa, m0 + 4 * mq);
+        if (!((S.am >> e) & 1u)) v = zero4();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Ab[(4 * mq + j) * LDK + kk] = v[j];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < RB; ++e) {
+      const int idx = t + NT * e;
+      f32x4 v = S.b[e];
+      if constexpr (BKC) {
+        const int n = idx >> 3, kq = idx & 7;
+        if (!((S.bm >> e) & 1u)) v = zero4();
+        if (n < BN) *reinterpret_cast<f32x4*>(Bb + n * LDK + 4 * kq) = v;
+      } else {
+        constexpr int NQ = BN / 4;
+        const int nq = idx % NQ, kk = idx / NQ;
+        if constexpr (XFB == CV_XF_BNRELU) v = xform4<XFB>(v, v, cB, nfb, P.f_cb.mod(n0 + 4 * nq));
+        if constexpr (XFB == CV_XF_BNBWD) v = xform4<XFB>(v, S.by[e], cB, nfb, P.f_cb.mod(n0 + 4 * nq));
+        if (!((S.bm >> e) & 1u)) v = zero4();
+        if (OP == OP_WGRAD && ((S.bone >> e) & 1u)) v = f32x4{1.f, 0.f, 0.f, 0.f};
+        if (kk < BK) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Bb[(4 * nq + j) * LDK + kk] = v[j];
+        }
+      }
+    }
+  };
+
+  // ---------------- prologue: first D-1 tiles in flight, then the BN constants
+  Stage stg[D];
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) fetch(stg[d], kbeg + min(d, nt - 1) * BK);
+
+  double* fold_scratch = reinterpret_cast<double*>(As);
+  static_assert(2 * BM * LDK * sizeof(float) >= 4 * NT * sizeof(double), "fold scratch");
+  if constexpr (XA != CV_XF_NONE) {
+    if (bn1d) {
+      for (int idx = t; idx < kend - kbeg; idx += NT) {
+        int f = kbeg + idx;
+        if (P.a_pix > 1) {
+          const int pix = f / P.a_ch, c = f - pix * P.a_ch;
+          f = c * P.a_pix + pix;
+        }
+        if constexpr (XA == CV_XF_BNRELU) {
+          const BnFwdC k = bn_fwd_const(P.a.bn, f);
+          cA[idx] = k.sc;
+          cA[nfa + idx] = k.mu;
+          cA[2 * nfa + idx] = k.be;
+        } else {
+          const BnBwdC k = bn_bwd_const(P.a.bn, f);
+          cA[idx] = k.sc;
+          cA[nfa + idx] = k.c1;
+          cA[2 * nfa + idx] = k.mu;
+          cA[3 * nfa + idx] = k.istd;
+          cA[4 * nfa + idx] = k.c2;
+        }
+      }
+    } else {
+      fill_soa<XA>(P.a.bn, nfa, cA, fold_scratch);
+    }
+  }
+  if constexpr (XFB != CV_XF_NONE) fill_soa<XFB>(P.b.bn, nfb, cB, fold_scratch);
+  if constexpr (EPI == CV_STAT_BWD) {
+    BnFwdC* d = reinterpret_cast<BnFwdC*>(cE);
+    bn_fold<NT>(P.ep.ebn, false, fold_scratch, [&](int f, double s, double q, double, double) {
+      if (f < P.ce_n) d[f] = bn_fwd_const_s(P.ep.ebn, f, s, q);
+    });
+  }
+  __syncthreads();
+  store(stg[0], 0);
+  __syncthreads();
+  CV_STAMP(st1);
+
+  // ---------------- main loop: one barrier per K tile, D-1 tiles of loads in flight
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = zero4();
+
+  const int fr = lane & 15, fk = 4 * (lane >> 4);
+  const float* Af = As + (wm * TM + fr) * LDK + fk;
+  const float* Bf = Bs + (wn * TN + fr) * LDK + fk;
+  auto mma = [&](int buf) {
+    const float* Ab = Af + buf * BM * LDK;
+    const float* Bb = Bf + buf * BN * LDK;
+    f32x4 av[BK / 16][FM], bv[BK / 16][FN];
+#pragma unroll
+    for (int kc = 0; kc < BK / 16; ++kc) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) av[kc][i] = lds4(Ab + i * 16 * LDK + kc * 16);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bv[kc][j] = lds4(Bb + j * 16 * LDK + kc * 16);
+    }
+#pragma unroll
+    for (int kc = 0; kc < BK / 16; ++kc)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc][i][s], bv[kc][j][s], acc[i][j], 0, 0, 0);
+  };
+  // Steady state: whole groups of D tiles with no exits inside the unrolled group (an exit would
+  // merge control flow and force conservative vmcnt waits); each step fetches tile tt+D-1 (clamped).
+  int tt = 0;
+  for (; tt + D <= nt; tt += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      fetch(stg[(d + D - 1) % D], kbeg + min(tt + d + D - 1, nt - 1) * BK);
+      mma((tt + d) & 1);
+      if (tt + d + 1 < nt) store(stg[(d + 1) % D], (tt + d + 1) & 1);
+      __syncthreads();
+    }
+  }
+  // Tail: the remaining r < D tiles are already staged (slots 0..r-1); no more loads.
+  const int rem = nt - tt;
+#pragma unroll
+  for (int r = 1; r < D; ++r) {
+    if (rem == r) {
+#pragma unroll
+      for (int d = 0; d < r; ++d) {
+        mma((tt + d) & 1);
+        if (d + 1 < r) store(stg[(d + 1) % D], (tt + d + 1) & 1);
+        __syncthreads();
+      }
+    }
+  }
+  CV_STAMP(st2);
+
+  // ---------------- epilogue (same semantics as the generic kernel)
+  constexpr bool STATS = EPI != CV_STAT_NONE;
+  float s1[FN], s2[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * TN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        float v = acc[i][j][r];
+        if (row >= M || col >= N) continue;
+        if constexpr (OP == OP_WGRAD) {
+          if (P.part) {
+            P.part[((size_t)bz * M + row) * N + col] = v;
+            continue;
+          }
+          const int tap = P.f_cb.div(col), c = col - tap * g.cb;
+          float* dst = (col >= P.N) ? P.gbias + row : P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap;
+          if (gridDim.z == 1) *dst += v;
+          else atomicAdd(dst, v);
+          continue;
+        } else {
+          size_t off;
+          if constexpr (OP == OP_GATHER) {
+            off = (size_t)row * g.cs + col;
+          } else if constexpr (OP == OP_SCATTER) {
+            const int hw = cy * cx;
+            const int nimg = f_cycx.div(row), rem = row - nimg * hw;
+            const int ty = f_cx.div(rem), tx = rem - ty * cx;
+            const int yb = yb0 + g.s * ty, xb = xb0 + g.s * tx;
+            off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + col;
+          } else {
+            const int oc = (P.o_pix > 1) ? P.f_opix.mod(col) * P.o_ch + P.f_opix.div(col) : col;
+            off = (size_t)row * P.ldo + oc;
+          }
+          if (P.bias && (!P.accumulate || bz == 0)) v += P.bias[col];
+          if (P.accumulate) {
+            atomicAdd(P.out + off, v);
+            continue;
+          }
+          if constexpr (EPI == CV_STAT_BWD) {
+            const int f = P.f_sdiv.div(col);
+            const float yv = P.ep.ey[off];
+            const BnFwdC k = reinterpret_cast<const BnFwdC*>(cE)[f];
+            if (P.ep.erelu && bn_out(yv, k) <= 0.f) v = 0.f;
+            P.out[off] = v;
+            s1[j] += v;
+            s2[j] += v * ((yv - k.mu) * k.istd);
+          } else {
+            P.out[off] = v;
+            if constexpr (STATS) {
+              s1[j] += v;
+              s2[j] += v * v;
+            }
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (OP != OP_WGRAD && STATS) {
+    if (!P.accumulate) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        s1[j] += __shfl_xor(s1[j], 16, 64);
+        s1[j] += __shfl_xor(s1[j], 32, 64);
+        s2[j] += __shfl_xor(s2[j], 16, 64);
+        s2[j] += __shfl_xor(s2[j], 32, 64);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = wn * TN + j * 16 + lane;
+          red[wm * BN + c] = s1[j];
+          red[WM * BN + wm * BN + c] = s2[j];
+        }
+      }
+      __syncthreads();
+      if (t < BN) {
+        const int col = n0 + t;
+        if (col < N) {
+          double a = 0.0, b = 0.0;
+#pragma unroll
+          for (int w = 0; w < WM; ++w) {
+            a += (double)red[w * BN + t];
+            b += (double)red[WM * BN + w * BN + t];
+          }
+          const int f = P.f_sdiv.div(col);
+          const int C = (EPI == CV_STAT_BWD) ? P.ce_n : P.ep.ebn.C;
+          const int repl = hw_id % CV_STAT_REPL(C);
+          double* so = P.ep.stat_out + (size_t)repl * 2 * C;
+          atomic_add_f64(so + f, a);
+          atomic_add_f64(so + C + f, b);
+        }
+      }
+    }
+  }
+#ifdef CV_STAMPS
+  if (t == 0 && g_stamps) {
+    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime();
+    unsigned long long* o = g_stamps + (size_t)hw_id * 8;
+    o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = mt0; o[5] = mt1;
+    o[6] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    o[7] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+  }
+#endif
+}
+
+#ifndef CV_FAST_DEPTH
+#define CV_FAST_DEPTH 3
+#endif
+
+template <int OP, int BM, int BN, int XA, int XB, int EPI>
+int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
+  constexpr int XFB = (OP == OP_WGRAD) ? XB : CV_XF_NONE;
+  const bool bn1d = (OP == OP_DENSE) && XA != CV_XF_NONE && a.ca_n == a.K;
+  const int nfa = (XA == CV_XF_NONE) ? 0 : (bn1d ? a.kchunk : a.ca_n);
+  const int nfb = (XFB == CV_XF_NONE) ? 0 : a.cb_n;
+  const size_t lds = fast_lds_floats(BM, BN, soa_arrays<XA>() * nfa, soa_arrays<XFB>() * nfb,
+                                     EPI == CV_STAT_BWD ? 4 * a.ce_n : 0) * sizeof(float);
+  CV_REQUIRE(lds <= 160 * 1024, "gemm: LDS request %zu bytes exceeds 160 KiB", lds);
+  auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, CV_FAST_DEPTH>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      cv::set_error("gemm: LDS carve-out of %zu bytes refused: %s", lds, hipGetErrorString(e));
+      return 1;
+    }
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
+  CV_LAUNCH_CHECK("gemm");
+  return 0;
+}
+
+// dispatch over the transform / epilogue modes of one (op, tile)
+template <int OP, int BM, int BN>
+int dispatch_modes(const Args& a, int xb, dim3 grid, hipStream_t st) {
+  const int xa = a.a.xf, ep = a.ep.stat_mode;
+#define CV_FAST_EP(XA_, XB_)                                                            \
+  if (ep == CV_STAT_NONE) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE>(a, grid, st); \
+  if (ep == CV_STAT_FWD) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_FWD>(a, grid, st);   \
+  return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_BWD>(a, grid, st);
+#define CV_FAST_XA(XB_)                        \
+  if (xa == CV_XF_NONE) { CV_FAST_EP(CV_XF_NONE, XB_) } \
+  if (xa == CV_XF_BNRELU) { CV_FAST_EP(CV_XF_BNRELU, XB_) } \
+  CV_FAST_EP(CV_XF_BNBWD, XB_)
+  if constexpr (OP == OP_WGRAD) {  // no epilogue statistics; B transform
+#undef CV_FAST_EP
+#define CV_FAST_EP(XA_, XB_) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE>(a, grid, st);
+    if (xb == CV_XF_NONE) { CV_FAST_XA(CV_XF_NONE) }
+    if (xb == CV_XF_BNRELU) { CV_FAST_XA(CV_XF_BNRELU) }
+    CV_FAST_XA(CV_XF_BNBWD)
+  } else if constexpr (OP == OP_DENSE) {
+#undef CV_FAST_EP
+#define CV_FAST_EP(XA_, XB_)                                                            \
+  if (ep == CV_STAT_NONE) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE>(a, grid, st); \
+  if (ep == CV_STAT_FWD) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_FWD>(a, grid, st);   \
+  return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_BWD>(a, grid, st);
+    if (xb == DB_KCONT) { CV_FAST_XA(DB_KCONT) }
+    if (xb == DB_NCONT) { CV_FAST_XA(DB_NCONT) }
+    CV_FAST_XA(DB_KPERM)
+  } else {
+    CV_FAST_XA(0)
+  }
+#undef CV_FAST_EP
+#undef CV_FAST_XA
+}
+
+template <int OP>
+int dispatch_tiles(const Args& a, int xb, int BM, int BN, dim3 grid, hipStream_t st) {
+  if (BM == 64 && BN == 16) return dispatch_modes<OP, 64, 16>(a, xb, grid, st);
+  if (BM == 64 && BN == 32) return dispatch_modes<OP, 64, 32>(a, xb, grid, st);
+  if (BM == 64 && BN == 64) return dispatch_modes<OP, 64, 64>(a, xb, grid, st);
+  if constexpr (OP != OP_DENSE) {
+    if (BM == 128 && BN == 16) return dispatch_modes<OP, 128, 16>(a, xb, grid, st);
+    if (BM == 128 && BN == 32) return dispatch_modes<OP, 128, 32>(a, xb, grid, st);
+    if (BM == 128 && BN == 64) return dispatch_modes<OP, 128, 64>(a, xb, grid, st);
+  }
+  return -1;
+}
+
+}  // namespace fast
+}  // namespace cv

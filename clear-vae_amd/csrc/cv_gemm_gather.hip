@@ -1,0 +1,19 @@
+// GATHER instances of the specialised implicit-GEMM core (cv_gemm.hpp); one translation
+// unit per op so the instances compile in parallel.
+#include "cv_gemm.hpp"
+
+namespace cv {
+
+int gemm_fast_gather(const Args& a, int BM, int BN, dim3 grid, hipStream_t st) {
+  if ((a.g.cb & 3) || a.a.nchw || (a.g.cs & 3)) return -1;
+  // 32-bit element offsets in the kernel
+  if ((long)a.g.n * a.g.hb * a.g.wb * a.g.cb >= (1L << 31) || (long)a.g.n * a.g.hs * a.g.ws * a.g.cs >= (1L << 31))
+    return -1;
+  return fast::dispatch_tiles<OP_GATHER>(a, 0, BM, BN, grid, st);
+}
+
+}  // namespace cv
+
+#ifdef CV_STAMPS
+CV_STAMPS_SETTER(cv_debug_set_stamps_gather)
+#endif

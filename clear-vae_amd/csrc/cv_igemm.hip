@@ -22,88 +22,9 @@
 // are pre-packed once per step (cv_pack_conv_weights) into GEMM-native [K][N] rows, so the B
 // operand is a coalesced float4 stream with no index arithmetic; activation gathers are float4
 // along channels with all integer division hoisted to once per row (rows) or once per K tile.
-#include "cv_common.hpp"
+#include "cv_igemm.hpp"
 
 namespace cv {
-
-constexpr int BK = 32;
-#ifndef CV_DEPTH
-#define CV_DEPTH 2  // register-ring depth (tiles staged ahead + 1); 3 measured slower (occupancy)
-#endif
-constexpr int NT = 256;
-
-enum { OP_GATHER = 0, OP_SCATTER = 1, OP_WGRAD = 2, OP_DENSE = 3 };
-
-
-struct Args {
-  int op;
-  Geo g;
-  cv_operand a;        // GATHER: big-grid input; SCATTER: small-grid input; WGRAD: small-grid; DENSE: A
-  cv_operand b;        // WGRAD: big-grid operand
-  const float* w;      // GATHER: packed [tap][cb][cs]; SCATTER: packed [tap][cs][cb]; DENSE: Linear weight
-  int wlayout;         // DENSE: 0 -> W[col*ldb + k], 1 -> W[k*ldb + col]
-  int ldb;
-  const float* bias;
-  float* gbias;        // WGRAD: bias gradient via an extra all-ones B column
-  float* part;         // WGRAD split-K: partial tiles [split][M][N(+1)] (else fp32 atomics)
-  float* out;
-  int accumulate;      // atomicAdd into out (split-K)
-  cv_epilogue ep;
-  int M, N, K;         // GEMM sizes (SCATTER: per class sizes computed in-kernel; N excludes bias col)
-  int kchunk;          // K elements per split (multiple of BK)
-  int lda, a_pix, a_ch;      // DENSE: A row stride; NCHW-flatten permutation of A columns (a_pix=1: none)
-  int ldo, o_pix, o_ch;      // DENSE: out row stride; permutation of output columns
-  int ca_n, cb_n, ce_n;      // feature counts of a / b / epilogue BN constants (0 = unused)
-  // fast divisors (filled by finalize_divs at launch)
-  FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
-};
-
-// ------------------------------------------------------------------ operand transform helpers
-struct XfA {
-  const BnFwdC* f;
-  const BnBwdC* bw;
-};
-
-__device__ __forceinline__ float xf_apply(const cv_operand& o, const XfA& c, int ch, float x, float y) {
-  if (o.xf == CV_XF_BNRELU) return bn_relu(x, c.f[ch]);
-  if (o.xf == CV_XF_BNBWD) return bn_bwd(x, y, c.bw[ch]);
-  return x;
-}
-
-__device__ __forceinline__ float4 xf_apply4(const cv_operand& o, const XfA& c, int ch0, float4 v, float4 yy) {
-  if (o.xf == CV_XF_NONE) return v;
-  v.x = xf_apply(o, c, ch0 + 0, v.x, yy.x);
-  v.y = xf_apply(o, c, ch0 + 1, v.y, yy.y);
-  v.z = xf_apply(o, c, ch0 + 2, v.z, yy.z);
-  v.w = xf_apply(o, c, ch0 + 3, v.w, yy.w);
-  return v;
-}
-
-// BN constants of an operand into LDS (block-cooperative replica fold; scratch: 4*NT doubles)
-__device__ __forceinline__ void fill_consts(const cv_operand& o, int nfeat, float* lds, double* scratch, XfA& c) {
-  c.f = reinterpret_cast<const BnFwdC*>(lds);
-  c.bw = reinterpret_cast<const BnBwdC*>(lds);
-  if (o.xf == CV_XF_BNRELU) {
-    BnFwdC* d = reinterpret_cast<BnFwdC*>(lds);
-    bn_fold<NT>(o.bn, false, scratch, [&](int f, double s, double q, double, double) {
-      if (f < nfeat) d[f] = bn_fwd_const_s(o.bn, f, s, q);
-    });
-  } else if (o.xf == CV_XF_BNBWD) {
-    BnBwdC* d = reinterpret_cast<BnBwdC*>(lds);
-    bn_fold<NT>(o.bn, true, scratch, [&](int f, double s, double q, double gs, double gq) {
-      if (f < nfeat) d[f] = bn_bwd_const_s(o.bn, f, s, q, gs, gq);
-    });
-  }
-}
-
-__host__ __device__ inline int xf_floats(int xf, int nfeat) {
-  if (xf == CV_XF_BNRELU) return 4 * nfeat;
-  if (xf == CV_XF_BNBWD) return 5 * nfeat;
-  return 0;
-}
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ float4 z4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 // ------------------------------------------------------------------ the kernel
 // Operand staging: global -> registers (raw values, a validity mask) -> [after the MFMAs of the
@@ -144,6 +65,10 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   float* cstB = cstA + xf_floats(P.a.xf, bn1d ? P.kchunk : P.ca_n);
   float* cstE = cstB + xf_floats(P.b.xf, P.cb_n);
 
+  CV_STAMP(st0);
+#ifdef CV_STAMPS
+  const unsigned long long mt0 = __builtin_amdgcn_s_memtime();
+#endif
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const Geo& g = P.g;
@@ -569,6 +494,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
   storeA(stg[0], As, kbeg);
   storeB(stg[0], Bs);
   __syncthreads();
+  CV_STAMP(st1);
   for (int tb = 0; tb < nt; tb += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -605,6 +531,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
     }
   }
 
+  CV_STAMP(st2);
   // ---------------- epilogue
   const bool stats = P.ep.stat_mode != CV_STAT_NONE;
   float s1[FN], s2[FN];
@@ -705,6 +632,15 @@ __global__ __launch_bounds__(NT) void igemm_kernel(const Args P) {
       }
     }
   }
+#ifdef CV_STAMPS
+  if (t == 0 && g_stamps) {
+    const unsigned long long st3 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime();
+    unsigned long long* o = g_stamps + (size_t)hw_id * 8;
+    o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = mt0; o[5] = mt1;
+    o[6] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    o[7] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ weight packing
@@ -828,6 +764,9 @@ static void finalize_divs(Args& a) {
   a.f_s = FDiv::make(a.g.s);
 }
 
+// 1: route every call to the generic kernel (kernel-variant comparisons in tests only)
+static int g_force_generic = 0;
+
 static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
   finalize_divs(a);
   const int Ntot = a.N + ((a.op == OP_WGRAD && a.gbias) ? 1 : 0);
@@ -835,6 +774,16 @@ static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
   dim3 grid(gx, gy, gz);
   CV_REQUIRE(gx > 0 && gy > 0 && gz > 0, "igemm: empty grid");
   CV_REQUIRE(gx < (1 << 30) && gy < 65536 && gz < 65536, "igemm: grid too large");
+  if (!g_force_generic) {  // the specialised core serves every vectorisable call
+    int r = -1;
+    switch (a.op) {
+      case OP_GATHER: r = gemm_fast_gather(a, BM_, BN_, grid, st); break;
+      case OP_SCATTER: r = gemm_fast_scatter(a, BM_, BN_, grid, st); break;
+      case OP_WGRAD: r = gemm_fast_wgrad(a, BM_, BN_, grid, st); break;
+      default: r = gemm_fast_dense(a, BM_, BN_, grid, st); break;
+    }
+    if (r >= 0) return r;
+  }
   switch (a.op) {
     case OP_GATHER: return launch_op<OP_GATHER>(a, BM_, BN_, grid, st);
     case OP_SCATTER: return launch_op<OP_SCATTER>(a, BM_, BN_, grid, st);
@@ -1072,6 +1021,16 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
 }  // namespace cv
 
 using namespace cv;
+
+extern "C" int cv_debug_force_generic_gemm(int on) {
+  const int prev = g_force_generic;
+  g_force_generic = on ? 1 : 0;
+  return prev;
+}
+
+#ifdef CV_STAMPS
+CV_STAMPS_SETTER(cv_debug_set_stamps)
+#endif
 
 extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream) {
   clear_error();

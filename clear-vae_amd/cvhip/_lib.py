@@ -212,6 +212,7 @@ _SIGS = {
     "cv_zero": (c_int, [c_void_p, c_size_t, c_void_p]),
     "cv_last_error": (ctypes.c_char_p, []),
     "cv_version": (c_int, []),
+    "cv_debug_force_generic_gemm": (c_int, [c_int]),
 }
 
 EXPORTED = tuple(_SIGS)

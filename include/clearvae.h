@@ -288,6 +288,9 @@ int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dgamma, float*
 int cv_zero(void* ptr, size_t bytes, cv_stream_t stream);
 const char* cv_last_error(void);
 int cv_version(void);
+/* test hook: 1 routes every conv/linear GEMM to the generic implicit-GEMM kernel instead of the
+ * specialised core (both compute the same contraction); returns the previous setting */
+int cv_debug_force_generic_gemm(int on);
 
 #ifdef __cplusplus
 }

@@ -87,9 +87,19 @@ def _packed(lib_mod, W, tr):
     return (sca, gat) if tr else (gat, sca)
 
 
+@pytest.fixture(params=["core", "generic"])
+def gemm_kernel(request):
+    """Run a test on the specialised GEMM core (default path) and on the generic kernel."""
+    from cvhip import _lib
+
+    prev = _lib.lib().cv_debug_force_generic_gemm(1 if request.param == "generic" else 0)
+    yield request.param
+    _lib.lib().cv_debug_force_generic_gemm(prev)
+
+
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "T" * g[1] + f"{g[2]}x{g[3]}-{g[4]}x{g[5]}k{g[6]}")
 @pytest.mark.parametrize("xf", ["none", "bn"])
-def test_conv_fwd_bwd_wgrad(geom, xf):
+def test_conv_fwd_bwd_wgrad(geom, xf, gemm_kernel):
     from cvhip import _lib
 
     n, tr, cin, hin, cout, hout, k, s, p = geom
@@ -188,7 +198,7 @@ def test_conv_fwd_bwd_wgrad(geom, xf):
 
 @pytest.mark.parametrize("geom", [g for g in GEOMS if g[2] not in (1, 3)],
                          ids=lambda g: "T" * g[1] + f"{g[2]}x{g[3]}-{g[4]}x{g[5]}k{g[6]}")
-def test_backward_data_stat_epilogue(geom):
+def test_backward_data_stat_epilogue(geom, gemm_kernel):
     """cv_conv_backward_data with CV_STAT_BWD: the stored tensor is dz = dx * [BN+ReLU active] and the
     fp64 sums are (sum dz, sum dz*xhat) of the BN layer that feeds this conv."""
     from cvhip import _lib
