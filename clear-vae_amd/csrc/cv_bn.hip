@@ -324,6 +324,7 @@ __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int p
     atomic_add_f64(gstat + (size_t)repl * 2 * F + fidx[t], a);
     atomic_add_f64(gstat + (size_t)repl * 2 * F + F + fidx[t], q);
   }
+  __shared__ double scratch[4 * 256];
 }
 
 template <int KPT>

@@ -236,6 +236,55 @@ __device__ __forceinline__ void bn_fold(const cv_bn& b, bool with_g, double* scr
   __syncthreads();
 }
 
+// Last-arriver finalisation of a BatchNorm layer's constants (include/clearvae.h, cv_bn.ticket).
+// EVERY thread of EVERY workgroup of a launch that produces BN sums calls this exactly once, after its
+// own statistics atomics, in uniform control flow.  The last workgroup to arrive folds the replicas
+// (`produced` = the sums this launch accumulated: the forward sums, or the backward sums with b.stat
+// holding the forward ones) and writes cfwd = [sc][mu][beta][istd] or cbwd = [sc][c1][mu][istd][c2].
+// Hand-off (cdna_hip_programming.md, Guideline 16): every wave drains its atomics (vmcnt(0)) before
+// the barrier, one lane adds to the ticket (agent scope), the electee acquires before its loads.
+// scratch: >= 4*NT doubles of LDS that are no longer live; flag: one int of LDS.
+template <int NT>
+__device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, bool bwd, double* scratch, int* flag) {
+  float* out = bwd ? b.cbwd : b.cfwd;
+  if (!b.ticket || !out || !b.train || !produced) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned prev =
+        __hip_atomic_fetch_add(b.ticket + (bwd ? 1 : 0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (prev == nblk - 1) ? 1 : 0;
+    if (prev == nblk - 1) {  // acquire once, before the barrier that publishes the flag to the block
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (bwd) b.gstat = produced;
+  else b.stat = produced;
+  const int C = b.C;
+  if (!bwd) {
+    bn_fold<NT>(b, false, scratch, [&](int f, double s, double q, double, double) {
+      const BnFwdC k = bn_fwd_const_s(b, f, s, q);
+      out[f] = k.sc;
+      out[C + f] = k.mu;
+      out[2 * C + f] = k.be;
+      out[3 * C + f] = k.istd;
+    });
+  } else {
+    bn_fold<NT>(b, true, scratch, [&](int f, double s, double q, double gs, double gq) {
+      const BnBwdC k = bn_bwd_const_s(b, f, s, q, gs, gq);
+      out[f] = k.sc;
+      out[C + f] = k.c1;
+      out[2 * C + f] = k.mu;
+      out[3 * C + f] = k.istd;
+      out[4 * C + f] = k.c2;
+    });
+  }
+}
+
 // (x - mu) first: the subtraction is exact for x near mu, so the sign test of a near-zero BN output
 // (the ReLU mask) agrees with an fp64 evaluation far more often than x*sc + (beta - mu*sc) does.
 __device__ __forceinline__ float bn_out(float x, BnFwdC k) { return fmaf(x - k.mu, k.sc, k.be); }

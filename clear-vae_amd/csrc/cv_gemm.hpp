@@ -53,6 +53,31 @@ __device__ __forceinline__ f32x4 xform4(f32x4 x, f32x4 y, const float* c, int nf
   return x;
 }
 
+// per-thread register copy of the constants of one channel quad (BNRELU: sc, mu, be; BNBWD: sc, c1,
+// mu, istd, c2), reloaded only when the quad changes
+struct XC {
+  f32x4 k[5];
+};
+template <int XF>
+__device__ __forceinline__ XC load_xc(const float* c, int nf, int ch) {
+  XC r;
+#pragma unroll
+  for (int q = 0; q < soa_arrays<XF>(); ++q) r.k[q] = lds4(c + q * nf + ch);
+  return r;
+}
+template <int XF>
+__device__ __forceinline__ f32x4 apply_xc(f32x4 x, f32x4 y, const XC& c) {
+  if constexpr (XF == CV_XF_BNRELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = fmaxf(fmaf(x[j] - c.k[1][j], c.k[0][j], c.k[2][j]), 0.f);
+  } else if constexpr (XF == CV_XF_BNBWD) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      x[j] = c.k[0][j] * (x[j] - c.k[1][j] - (y[j] - c.k[2][j]) * c.k[3][j] * c.k[4][j]);
+  }
+  return x;
+}
+
 template <int XF>
 __device__ __forceinline__ void fill_soa(const cv_bn& bn, int nf, float* dst, double* scratch) {
   if constexpr (XF == CV_XF_BNRELU) {
@@ -76,6 +101,35 @@ __device__ __forceinline__ void fill_soa(const cv_bn& bn, int nf, float* dst, do
       }
     });
   }
+}
+
+// Finalised constants of a train-mode layer (cv_bn.cfwd / cbwd, written by the producer's last
+// workgroup): a float4 copy into LDS instead of the replica fold.  The SoA order of cfwd starts with
+// [sc][mu][beta] and cbwd is [sc][c1][mu][istd][c2], exactly the LDS images above.
+template <int XF>
+__device__ __forceinline__ bool load_soa(const cv_bn& bn, int nf, float* dst) {
+  const float* src = (XF == CV_XF_BNRELU) ? bn.cfwd : bn.cbwd;
+  if (!bn.train || !src || !bn.ticket || nf != bn.C) return false;
+  // the constant loads are issued with the ticket load (a zero ticket: the producer did not
+  // finalise, and the fold runs instead)
+  constexpr int MQ4 = 3;
+  const int n4 = soa_arrays<XF>() * nf / 4;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+  f32x4 tmp[MQ4];
+#pragma unroll
+  for (int q = 0; q < MQ4; ++q) {
+    const int i = threadIdx.x + q * NT;
+    tmp[q] = s4[i < n4 ? i : 0];
+  }
+  if (bn.ticket[XF == CV_XF_BNRELU ? 0 : 1] == 0u) return false;
+  f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+#pragma unroll
+  for (int q = 0; q < MQ4; ++q) {
+    const int i = threadIdx.x + q * NT;
+    if (i < n4) d4[i] = tmp[q];
+  }
+  for (int i = threadIdx.x + MQ4 * NT; i < n4; i += NT) d4[i] = s4[i];
+  return true;
 }
 
 // DENSE B modes (the XB slot of a DENSE instance)
@@ -128,6 +182,14 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
   const int wm = wid / WN, wn = wid % WN;
   const Geo& g = P.g;
 
+  // producer side of the BN constants hand-off: every workgroup arrives once (early exits too)
+  auto finalize = [&](bool) {
+    if constexpr (EPI != CV_STAT_NONE) {
+      bn_finalize<NT>(P.ep.ebn, P.ep.stat_out, EPI == CV_STAT_BWD, reinterpret_cast<double*>(As),
+                      reinterpret_cast<int*>(As + 4096));
+    }
+  };
+
   // ---------------- block -> (m0, n0, k-range, class): identical to the generic kernel
   const int gx = gridDim.x, gy = gridDim.y;
   const int nwg = gx * gy * gridDim.z;
@@ -159,46 +221,74 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
     M = g.n * cy * cx;
     K = nty * ntx * g.cs;
     kend = K;
-    if (m0 >= M) return;
+    if (m0 >= M) {
+      finalize(true);
+      return;
+    }
     f_cx = FDiv::make(cx);
     f_cycx = FDiv::make(cy * cx);
     f_ntx = FDiv::make(ntx);
   } else {
     kbeg = bz * P.kchunk;
     kend = min(K, kbeg + P.kchunk);
-    if (kbeg >= kend) return;
+    if (kbeg >= kend) {
+      finalize(true);
+      return;
+    }
   }
   const int nt = (kend - kbeg + BK - 1) / BK;
+  // GATHER / SCATTER visit K tiles tap-inner: tile j = (channel block j / ntap, tap j % ntap), so a
+  // thread's channel quad (and its BN constants) changes only every ntap tiles
+  const int ntap = (OP == OP_GATHER) ? g.kh * g.kw : (OP == OP_SCATTER ? (ntx > 0 ? K / g.cs : 1) : 1);
+  const FDiv f_ntap = FDiv::make(ntap);
+  const int CK = (OP == OP_GATHER) ? g.cb : g.cs;  // channels per tap of the K index
 
-  // ---------------- per-thread A rows (row-oriented ops): rows (t>>3) + 32 i, k quad t & 7
+  // ---------------- per-thread A rows (row-oriented ops): rows (t>>3) + 32 i, k quad t & 7.
+  // GATHER / SCATTER: a K tile never straddles a tap (channels % BK == 0, checked on the host), so
+  // the tap of a tile is wave-uniform (scalar unit); per row we keep the element offset of tap 0,
+  // channel 0 (r_base, may be negative for padded rows) and a bitmask of the taps that land inside
+  // the image (r_vm), so a tile costs one add and one bit test per row.
   const int aq = t & 7, ar = t >> 3;
-  int r_n[RA], r_y[RA], r_x[RA];
-  bool r_ok[RA];
+  int r_base[RA];
+  unsigned r_vm[RA];
+  int cy0 = 0, cx0 = 0;
+  if constexpr (OP == OP_SCATTER) {
+    cy0 = (yb0 + g.p - ry) / g.s;  // small row of class tap jy = 0 is cy0 + ty (exact division)
+    cx0 = (xb0 + g.p - rx) / g.s;
+  }
   if constexpr (ROWS) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int r = m0 + ar + 32 * i;
-      r_ok[i] = r < M;
-      const int rr = r_ok[i] ? r : 0;
-      if (OP == OP_GATHER) {
+      const bool ok = r < M;
+      const int rr = ok ? r : 0;
+      unsigned vm = 0;
+      if constexpr (OP == OP_GATHER) {
         const int hw = g.hs * g.ws;
-        r_n[i] = P.f_hws.div(rr);
-        const int rem = rr - r_n[i] * hw;
+        const int n = P.f_hws.div(rr);
+        const int rem = rr - n * hw;
         const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
-        r_y[i] = ys * g.s - g.p;
-        r_x[i] = xs * g.s - g.p;
-      } else if (OP == OP_SCATTER) {
+        const int y0 = ys * g.s - g.p, x0 = xs * g.s - g.p;
+        r_base[i] = ((n * g.hb + y0) * g.wb + x0) * g.cb;
+        for (int kh = 0; kh < g.kh; ++kh)
+          for (int kw = 0; kw < g.kw; ++kw)
+            if ((unsigned)(y0 + kh) < (unsigned)g.hb && (unsigned)(x0 + kw) < (unsigned)g.wb) vm |= 1u << (kh * g.kw + kw);
+      } else if constexpr (OP == OP_SCATTER) {
         const int hw = cy * cx;
-        r_n[i] = f_cycx.div(rr);
-        const int rem = rr - r_n[i] * hw;
+        const int n = f_cycx.div(rr);
+        const int rem = rr - n * hw;
         const int ty = f_cx.div(rem), tx = rem - ty * cx;
-        r_y[i] = yb0 + g.s * ty + g.p;
-        r_x[i] = xb0 + g.s * tx + g.p;
+        const int y0 = cy0 + ty, x0 = cx0 + tx;  // small pixel of class tap (0, 0)
+        r_base[i] = ((n * g.hs + y0) * g.ws + x0) * g.cs;
+        const int nty = ntx > 0 ? (K / g.cs) / ntx : 0;
+        for (int jy = 0; jy < nty; ++jy)
+          for (int jx = 0; jx < ntx; ++jx)
+            if ((unsigned)(y0 - jy) < (unsigned)g.hs && (unsigned)(x0 - jx) < (unsigned)g.ws) vm |= 1u << (jy * ntx + jx);
       } else {
-        r_n[i] = rr;
-        r_y[i] = 0;
-        r_x[i] = 0;
+        r_base[i] = rr * P.lda;
+        vm = 1u;
       }
+      r_vm[i] = ok ? vm : 0u;
     }
   }
 
@@ -213,10 +303,24 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
     f32x4 b[RB], by[BYY ? RB : 1];
     unsigned am, bm, bone;  // validity masks; bone: WGRAD bias-column slots
     int ach;                // channel index of the A transform constants
+    int cb0;                // GATHER / SCATTER: channel block of the tile (wave-uniform)
   };
 
   // ---------------- global -> registers (every load unconditional)
-  auto fetch = [&](Stage& S, int k0) {
+  auto fetch = [&](Stage& S, int j) {
+#if defined(CV_ABLATE) && CV_ABLATE == 2
+    j = 0;  // diagnostic build: every tile re-reads the first tile (L1/L2-hot)
+#endif
+    int k0, tap = 0, cb0 = 0;
+    if constexpr (OP == OP_GATHER || OP == OP_SCATTER) {
+      const int cblk = f_ntap.div(j);  // wave-uniform
+      tap = j - cblk * ntap;
+      cb0 = cblk * BK;
+      k0 = tap * CK + cb0;
+    } else {
+      k0 = kbeg + j * BK;
+    }
+    S.cb0 = cb0;
     S.am = 0;
     S.bm = 0;
     S.bone = 0;
@@ -226,31 +330,25 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
       const int kq = k0 + 4 * aq;
       const bool kok = kq < kend;
       if constexpr (OP == OP_GATHER) {
-        const int tap = P.f_cb.div(kq), c0 = kq - tap * g.cb;
         const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
-        S.ach = c0;
+        const int toff = (kh * g.wb + kw) * g.cb + cb0 + 4 * aq;
+        S.ach = cb0 + 4 * aq;
 #pragma unroll
         for (int i = 0; i < RA; ++i) {
-          const int yb = r_y[i] + kh, xb = r_x[i] + kw;
-          const bool ok = r_ok[i] && kok && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
-          int off = ((r_n[i] * g.hb + yb) * g.wb + xb) * g.cb + c0;
-          off = ok ? off : 0;
+          const bool ok = kok && ((r_vm[i] >> tap) & 1u);
+          const int off = ok ? r_base[i] + toff : 0;
           S.a[i] = g4(ax + off);
           if constexpr (AY) S.ay[i] = g4(ayp + off);
           S.am |= (ok ? 1u : 0u) << i;
         }
       } else if constexpr (OP == OP_SCATTER) {
-        const int tap = P.f_cs.div(kq), c0 = kq - tap * g.cs;
         const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
-        const int kh = ry + g.s * jy, kw = rx + g.s * jx;
-        S.ach = c0;
+        const int toff = cb0 + 4 * aq - (jy * g.ws + jx) * g.cs;
+        S.ach = cb0 + 4 * aq;
 #pragma unroll
         for (int i = 0; i < RA; ++i) {
-          const int py = r_y[i] - kh, px = r_x[i] - kw;  // multiples of s by construction
-          const int ys = P.f_s.div(max(py, 0)), xs = P.f_s.div(max(px, 0));
-          const bool ok = r_ok[i] && kok && py >= 0 && px >= 0 && ys < g.hs && xs < g.ws;
-          int off = ((r_n[i] * g.hs + ys) * g.ws + xs) * g.cs + c0;
-          off = ok ? off : 0;
+          const bool ok = kok && ((r_vm[i] >> tap) & 1u);
+          const int off = ok ? r_base[i] + toff : 0;
           S.a[i] = g4(ax + off);
           if constexpr (AY) S.ay[i] = g4(ayp + off);
           S.am |= (ok ? 1u : 0u) << i;
@@ -259,9 +357,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
         S.ach = bn1d ? kq - kbeg : (P.a_pix > 1 ? P.f_ach.mod(kq) : kq);
 #pragma unroll
         for (int i = 0; i < RA; ++i) {
-          const bool ok = r_ok[i] && kok;
-          int off = r_n[i] * P.lda + kq;
-          off = ok ? off : 0;
+          const bool ok = r_vm[i] && kok;
+          const int off = ok ? r_base[i] + kq : 0;
           S.a[i] = g4(ax + off);
           if constexpr (AY) S.ay[i] = g4(ayp + off);
           S.am |= (ok ? 1u : 0u) << i;
@@ -311,12 +408,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
         bool ok = kk < BK && k < kend && col < N;
         int off = 0;
         if constexpr (OP == OP_GATHER) {
-          off = k * g.cs + col;
+          off = k0 * g.cs + (kk * g.cs + col);
         } else if constexpr (OP == OP_SCATTER) {
-          const int tap = P.f_cs.div(k), c = k - tap * g.cs;
           const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
           const int kh = ry + g.s * jy, kw = rx + g.s * jx;
-          off = ((kh * g.kw + kw) * g.cs + c) * g.cb + col;
+          off = ((kh * g.kw + kw) * g.cs + cb0) * g.cb + (kk * g.cb + col);
         } else if constexpr (OP == OP_DENSE) {
           off = lf(k) * P.ldb + col;
         } else {  // WGRAD: B(k = small pixel, col = (tap, cb)) = T(big[gather(pix, tap)][cb])
@@ -341,15 +437,28 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
   };
 
   // ---------------- transform + registers -> LDS
+  XC xa, xb;        // register copies of the transform constants
+  int xa_cb0 = -1;  // channel block xa belongs to (GATHER / SCATTER)
   auto store = [&](Stage& S, int buf) {
     float* Ab = As + buf * BM * LDK;
     float* Bb = Bs + buf * BN * LDK;
     if constexpr (ROWS) {
+      if constexpr (XA != CV_XF_NONE && OP != OP_DENSE) {
+        if (S.cb0 != xa_cb0) {  // wave-uniform: a new channel block
+          xa = load_xc<XA>(cA, nfa, S.ach);
+          xa_cb0 = S.cb0;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
         f32x4 v = S.a[i];
-        if constexpr (XA == CV_XF_BNRELU) v = xform4<XA>(v, v, cA, nfa, S.ach);
-        if constexpr (XA == CV_XF_BNBWD) v = xform4<XA>(v, S.ay[i], cA, nfa, S.ach);
+        if constexpr (OP == OP_DENSE) {
+          if constexpr (XA == CV_XF_BNRELU) v = xform4<XA>(v, v, cA, nfa, S.ach);
+          if constexpr (XA == CV_XF_BNBWD) v = xform4<XA>(v, S.ay[i], cA, nfa, S.ach);
+        } else {
+          if constexpr (XA == CV_XF_BNRELU) v = apply_xc<XA>(v, v, xa);
+          if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[i], xa);
+        }
         if (!((S.am >> i) & 1u)) v = zero4();
         *reinterpret_cast<f32x4*>(Ab + (ar + 32 * i) * LDK + 4 * aq) = v;
       }
@@ -360,8 +469,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
         const int idx = t + NT * e;
         const int mq = idx % MQ, kk = idx / MQ;
         f32x4 v = S.a[e];
-        if constexpr (XA == CV_XF_BNRELU) v = xform4<XA>(v, v, cA, nfa, m0 + 4 * mq);
-        if constexpr (XA == CV_XF_BNBWD) v = xform4<XA>(v, S.ay[e], cA, nfa, m0 + 4 * mq);
+        if constexpr (XA == CV_XF_BNRELU) v = apply_xc<XA>(v, v, xa);
+        if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[e], xa);
         if (!((S.am >> e) & 1u)) v = zero4();
 #pragma unroll
         for (int j = 0; j < 4; ++j) Ab[(4 * mq + j) * LDK + kk] = v[j];
@@ -378,8 +487,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
       } else {
         constexpr int NQ = BN / 4;
         const int nq = idx % NQ, kk = idx / NQ;
-        if constexpr (XFB == CV_XF_BNRELU) v = xform4<XFB>(v, v, cB, nfb, P.f_cb.mod(n0 + 4 * nq));
-        if constexpr (XFB == CV_XF_BNBWD) v = xform4<XFB>(v, S.by[e], cB, nfb, P.f_cb.mod(n0 + 4 * nq));
+        if constexpr (XFB == CV_XF_BNRELU) v = apply_xc<XFB>(v, v, xb);
+        if constexpr (XFB == CV_XF_BNBWD) v = apply_xc<XFB>(v, S.by[e], xb);
         if (!((S.bm >> e) & 1u)) v = zero4();
         if (OP == OP_WGRAD && ((S.bone >> e) & 1u)) v = f32x4{1.f, 0.f, 0.f, 0.f};
         if (kk < BK) {
@@ -393,19 +502,28 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
   // ---------------- prologue: first D-1 tiles in flight, then the BN constants
   Stage stg[D];
 #pragma unroll
-  for (int d = 0; d < D - 1; ++d) fetch(stg[d], kbeg + min(d, nt - 1) * BK);
+  for (int d = 0; d < D - 1; ++d) fetch(stg[d], max(min(d, nt - 1), 0));
 
   double* fold_scratch = reinterpret_cast<double*>(As);
-  static_assert(2 * BM * LDK * sizeof(float) >= 4 * NT * sizeof(double), "fold scratch");
+  static_assert(2 * BM * LDK * sizeof(float) >= 4 * NT * sizeof(double) + 16, "fold scratch");
+#if defined(CV_ABLATE) && CV_ABLATE == 3
+  if (false)  // diagnostic build: no constants fold (garbage constants)
+#endif
+  {
   if constexpr (XA != CV_XF_NONE) {
     if (bn1d) {
+      const float* src = (XA == CV_XF_BNRELU) ? P.a.bn.cfwd : P.a.bn.cbwd;
+      const int C1 = P.a.bn.C;
       for (int idx = t; idx < kend - kbeg; idx += NT) {
         int f = kbeg + idx;
         if (P.a_pix > 1) {
           const int pix = f / P.a_ch, c = f - pix * P.a_ch;
           f = c * P.a_pix + pix;
         }
-        if constexpr (XA == CV_XF_BNRELU) {
+        if (P.a.bn.train && src && P.a.bn.ticket && P.a.bn.ticket[XA == CV_XF_BNRELU ? 0 : 1] != 0u) {
+#pragma unroll
+          for (int q = 0; q < soa_arrays<XA>(); ++q) cA[q * nfa + idx] = src[q * C1 + f];
+        } else if constexpr (XA == CV_XF_BNRELU) {
           const BnFwdC k = bn_fwd_const(P.a.bn, f);
           cA[idx] = k.sc;
           cA[nfa + idx] = k.mu;
@@ -419,21 +537,77 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
           cA[4 * nfa + idx] = k.c2;
         }
       }
-    } else {
+    } else if (!load_soa<XA>(P.a.bn, nfa, cA)) {
       fill_soa<XA>(P.a.bn, nfa, cA, fold_scratch);
     }
   }
-  if constexpr (XFB != CV_XF_NONE) fill_soa<XFB>(P.b.bn, nfb, cB, fold_scratch);
+  if constexpr (XFB != CV_XF_NONE) {
+    if (!load_soa<XFB>(P.b.bn, nfb, cB)) fill_soa<XFB>(P.b.bn, nfb, cB, fold_scratch);
+  }
   if constexpr (EPI == CV_STAT_BWD) {
     BnFwdC* d = reinterpret_cast<BnFwdC*>(cE);
-    bn_fold<NT>(P.ep.ebn, false, fold_scratch, [&](int f, double s, double q, double, double) {
-      if (f < P.ce_n) d[f] = bn_fwd_const_s(P.ep.ebn, f, s, q);
-    });
+    const cv_bn& eb = P.ep.ebn;
+    if (eb.train && eb.cfwd && eb.ticket && eb.C == P.ce_n && eb.ticket[0] != 0u) {
+      for (int f = t; f < P.ce_n; f += NT) {
+        BnFwdC k;
+        k.sc = eb.cfwd[f];
+        k.mu = eb.cfwd[eb.C + f];
+        k.be = eb.cfwd[2 * eb.C + f];
+        k.istd = eb.cfwd[3 * eb.C + f];
+        d[f] = k;
+      }
+    } else {
+      bn_fold<NT>(eb, false, fold_scratch, [&](int f, double s, double q, double, double) {
+        if (f < P.ce_n) d[f] = bn_fwd_const_s(eb, f, s, q);
+      });
+    }
+  }
   }
   __syncthreads();
+  if constexpr (OP == OP_WGRAD) {  // a thread's channel quads are fixed for the whole K range
+    if constexpr (XA != CV_XF_NONE) {
+      const int c0 = m0 + 4 * (t % (BM / 4));
+      xa = load_xc<XA>(cA, nfa, c0 < nfa ? c0 : 0);
+    }
+    if constexpr (XFB != CV_XF_NONE) {
+      const int col = n0 + 4 * (t % (BN / 4));
+      xb = load_xc<XFB>(cB, nfb, col < P.N ? P.f_cb.mod(col) : 0);
+    }
+  }
   store(stg[0], 0);
   __syncthreads();
   CV_STAMP(st1);
+
+  // ---------------- output element offsets; STAT_BWD prefetches the BN inputs at its outputs here,
+  // so their latency hides under the main loop instead of opening the epilogue
+  auto ep_off = [&](int row, int col) -> int {
+    if constexpr (OP == OP_GATHER) {
+      return row * g.cs + col;
+    } else if constexpr (OP == OP_SCATTER) {
+      const int hw = cy * cx;
+      const int nimg = f_cycx.div(row), rem = row - nimg * hw;
+      const int ty = f_cx.div(rem), tx = rem - ty * cx;
+      return ((nimg * g.hb + yb0 + g.s * ty) * g.wb + xb0 + g.s * tx) * g.cb + col;
+    } else {
+      const int oc = (P.o_pix > 1) ? P.f_opix.mod(col) * P.o_ch + P.f_opix.div(col) : col;
+      return row * P.ldo + oc;
+    }
+  };
+  float eyv[EPI == CV_STAT_BWD ? FM : 1][EPI == CV_STAT_BWD ? FN : 1][4];
+  if constexpr (EPI == CV_STAT_BWD && OP != OP_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wn * TN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          const bool ok = row < M && col < N;
+          eyv[i][j][r] = P.ep.ey[ok ? ep_off(row, col) : 0];
+        }
+      }
+  }
 
   // ---------------- main loop: one barrier per K tile, D-1 tiles of loads in flight
   f32x4 acc[FM][FN];
@@ -446,6 +620,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
   const float* Af = As + (wm * TM + fr) * LDK + fk;
   const float* Bf = Bs + (wn * TN + fr) * LDK + fk;
   auto mma = [&](int buf) {
+#if defined(CV_ABLATE) && CV_ABLATE == 1
+    return;  // diagnostic build: no fragment reads / MFMAs
+#endif
     const float* Ab = Af + buf * BM * LDK;
     const float* Bb = Bf + buf * BN * LDK;
     f32x4 av[BK / 16][FM], bv[BK / 16][FN];
@@ -472,7 +649,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
   for (; tt + D <= nt; tt += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      fetch(stg[(d + D - 1) % D], kbeg + min(tt + d + D - 1, nt - 1) * BK);
+      fetch(stg[(d + D - 1) % D], min(tt + d + D - 1, nt - 1));
       mma((tt + d) & 1);
       if (tt + d + 1 < nt) store(stg[(d + 1) % D], (tt + d + 1) & 1);
       __syncthreads();
@@ -522,19 +699,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
           else atomicAdd(dst, v);
           continue;
         } else {
-          size_t off;
-          if constexpr (OP == OP_GATHER) {
-            off = (size_t)row * g.cs + col;
-          } else if constexpr (OP == OP_SCATTER) {
-            const int hw = cy * cx;
-            const int nimg = f_cycx.div(row), rem = row - nimg * hw;
-            const int ty = f_cx.div(rem), tx = rem - ty * cx;
-            const int yb = yb0 + g.s * ty, xb = xb0 + g.s * tx;
-            off = ((size_t)(nimg * g.hb + yb) * g.wb + xb) * g.cb + col;
-          } else {
-            const int oc = (P.o_pix > 1) ? P.f_opix.mod(col) * P.o_ch + P.f_opix.div(col) : col;
-            off = (size_t)row * P.ldo + oc;
-          }
+          const int off = ep_off(row, col);
           if (P.bias && (!P.accumulate || bz == 0)) v += P.bias[col];
           if (P.accumulate) {
             atomicAdd(P.out + off, v);
@@ -542,7 +707,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
           }
           if constexpr (EPI == CV_STAT_BWD) {
             const int f = P.f_sdiv.div(col);
-            const float yv = P.ep.ey[off];
+            const float yv = eyv[i][j][r];
             const BnFwdC k = reinterpret_cast<const BnFwdC*>(cE)[f];
             if (P.ep.erelu && bn_out(yv, k) <= 0.f) v = 0.f;
             P.out[off] = v;
@@ -596,6 +761,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(const Args P) {
         }
       }
     }
+    finalize(true);
   }
 #ifdef CV_STAMPS
   if (t == 0 && g_stamps) {

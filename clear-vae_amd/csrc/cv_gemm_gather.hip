@@ -5,7 +5,7 @@
 namespace cv {
 
 int gemm_fast_gather(const Args& a, int BM, int BN, dim3 grid, hipStream_t st) {
-  if ((a.g.cb & 3) || a.a.nchw || (a.g.cs & 3)) return -1;
+  if ((a.g.cb % BK) || a.a.nchw || (a.g.cs & 3) || a.g.kh * a.g.kw > 32) return -1;
   // 32-bit element offsets in the kernel
   if ((long)a.g.n * a.g.hb * a.g.wb * a.g.cb >= (1L << 31) || (long)a.g.n * a.g.hs * a.g.ws * a.g.cs >= (1L << 31))
     return -1;

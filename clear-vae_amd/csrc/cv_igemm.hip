@@ -850,6 +850,7 @@ static int apply_epilogue(Args& a, const cv_epilogue* ep, int ncols, const char*
     CV_REQUIRE(ep->ebn.C == nf, "%s: STAT_BWD feature count %d != %d", what, ep->ebn.C, nf);
     a.ce_n = ep->ebn.C;
   } else {
+    CV_REQUIRE(!ep->ebn.ticket || ep->ebn.C == nf, "%s: STAT_FWD layer width %d != %d", what, ep->ebn.C, nf);
     a.ep.ebn.C = nf;
   }
   return 0;

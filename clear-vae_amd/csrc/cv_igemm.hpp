@@ -19,7 +19,7 @@ enum { OP_GATHER = 0, OP_SCATTER = 1, OP_WGRAD = 2, OP_DENSE = 3 };
 static __device__ unsigned long long* g_stamps;  // one per translation unit
 #define CV_STAMPS_SETTER(fn)                                                          \
   extern "C" int fn(void* buf) {                                                      \
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 1; \
+    return hipMemcpyToSymbol(HIP_SYMBOL(cv::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 1; \
   }
 #define CV_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
 #else

@@ -45,6 +45,9 @@ class cv_bn(ctypes.Structure):
         ("count", c_int),
         ("train", c_int),
         ("eps", c_float),
+        ("cfwd", c_void_p),
+        ("cbwd", c_void_p),
+        ("ticket", c_void_p),
     ]
 
 

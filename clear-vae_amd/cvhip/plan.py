@@ -286,11 +286,29 @@ class BNView:
         if not mod.affine or not mod.track_running_stats:
             raise NotImplementedError("BatchNorm without affine / running stats is not supported")
 
+    # finalised-constant slots (Workspace.__init__): cfwd [4C], cbwd [5C] fp32 and a ticket pair
+    cfwd: torch.Tensor | None = None
+    cbwd: torch.Tensor | None = None
+    ticket: int | None = None
+
+    # Producer-side finalisation of the BN constants (cv_bn.ticket, include/clearvae.h): a GEMM-core
+    # producer writes them from its last workgroup and consuming GEMMs load them instead of folding the
+    # replica sums.  It pays only where both sides are GEMM-core launches (Workspace sets fin_fwd /
+    # fin_bwd for those layers): stamped per-block timelines on the MNIST step put the consumer
+    # prologues at 7-10 -> 3.5-4.5 us, while finalising for a narrow-kernel consumer only adds the
+    # producer's last-workgroup tail (up to +20 us on a 1,568-workgroup launch).
+    FINALISE = True
+    fin_fwd = False
+    fin_bwd = False
+
     def cv(self, train: bool) -> cv_bn:
         m = self.mod
+        fin = train and self.ticket is not None and self.FINALISE
         return cv_bn(
             m.weight.data_ptr(), m.bias.data_ptr(), self.stat.data_ptr(), self.gstat.data_ptr(),
             m.running_mean.data_ptr(), m.running_var.data_ptr(), self.C, self.count, int(train), float(m.eps),
+            self.cfwd.data_ptr() if fin and self.fin_fwd else None, self.cbwd.data_ptr() if fin and self.fin_bwd else None,
+            self.ticket if fin and (self.fin_fwd or self.fin_bwd) else None,
         )
 
 
@@ -316,6 +334,7 @@ def ep_fwd(bnv: BNView) -> cv_epilogue:
     e = ep_none()
     e.stat_mode = STAT_FWD
     e.stat_out = bnv.stat.data_ptr()
+    e.ebn = bnv.cv(True)  # the producer's last workgroup finalises this layer's constants
     return e
 
 
@@ -394,8 +413,12 @@ class Workspace:
         # fp64 statistics arena: per BN layer [REPL,2,C] forward + [REPL,2,C] backward, plus scalars
         bns = spec.bn_layers
         counts = [n * c.h_out * c.w_out for c in spec.enc] + [n] + [n * c.h_out * c.w_out for c in spec.dec]
-        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 64
+        # (+ one 8-byte ticket pair per layer after the scalars: zeroed with the statistics)
+        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 64 + len(bns)
         self.stats = torch.zeros(tot, dtype=torch.float64, device=device)
+        # finalised BN constants (written by each layer's producing launch, read by the GEMM prologues)
+        r4 = lambda v: (v + 3) & ~3  # noqa: E731  (16-byte aligned slots)
+        self.bn_consts = torch.zeros(sum(r4(4 * b.num_features) + r4(5 * b.num_features) for b in bns), **f32)
         self.bnv = []
         o = 0
         for b, cnt in zip(bns, counts):
@@ -406,10 +429,24 @@ class Workspace:
             self.bnv.append(BNView(b, st, gs, cnt))
             o += 2 * sz
         self.scal = self.stats[o:o + 64]  # [0:REC_REPL] rec replicas (cv_output_loss), [32] mse work
-        self.rec = self.scal[0:_lib.REC_REPL]
+        oc = 0
+        for i, bv in enumerate(self.bnv):
+            C = bv.C
+            bv.cfwd = self.bn_consts[oc:oc + 4 * C]
+            bv.cbwd = self.bn_consts[oc + r4(4 * C):oc + r4(4 * C) + 5 * C]
+            oc += r4(4 * C) + r4(5 * C)
+            bv.ticket = self.stats.data_ptr() + 8 * (o + 64 + i)
+        # interior layers: produced and consumed by GEMM-core launches in both directions (the layers
+        # next to the image-facing convs and the BatchNorm1d are served by the narrow / BN kernels)
         self.bn_enc = self.bnv[: len(spec.enc)]
         self.bn_1d = self.bnv[len(spec.enc)]
         self.bn_dec = self.bnv[len(spec.enc) + 1:]
+        nd = len(spec.dec)
+        for i, bv in enumerate(self.bn_enc):
+            bv.fin_fwd = bv.fin_bwd = i >= 1 and bv.C % 32 == 0
+        for j, bv in enumerate(self.bn_dec):
+            bv.fin_fwd = bv.fin_bwd = j + 2 < nd and bv.C % 32 == 0
+        self.rec = self.scal[0:_lib.REC_REPL]
         if with_grad:
             self.g_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]
             self.dheads = torch.empty(n, 4 * d, **f32)

@@ -12,9 +12,11 @@
  *   - activations are NHWC fp32 ("pixels x channels" row-major); weights keep PyTorch's layouts
  *     (Conv2d [Cout][Cin][kh][kw], ConvTranspose2d [Cin][Cout][kh][kw], Linear [out][in]);
  *   - BatchNorm batch statistics are accumulated in fp64 by the producing kernel's epilogue into
- *     CV_STAT_REPL(C) replicas of [2][C] doubles (sum, sum of squares / sum dz, sum dz*xhat) and folded
- *     into per-channel constants by the consuming kernel's prologue (the normalised activation is
- *     never written to HBM);
+ *     CV_STAT_REPL(C) replicas of [2][C] doubles (sum, sum of squares / sum dz, sum dz*xhat); when the
+ *     layer carries a ticket (cv_bn.ticket), the last workgroup of the producing launch folds them into
+ *     per-channel constants (cv_bn.cfwd / cv_bn.cbwd) that consuming GEMMs load in their prologue,
+ *     otherwise each consumer folds the replicas itself (the normalised activation is never written
+ *     to HBM);
  *   - return value 0 = success; otherwise cv_last_error() describes the failure (host-side checks
  *     run before any launch, so a failing call enqueues nothing).
  */
@@ -47,6 +49,17 @@ typedef struct cv_bn {
   int count;                 /* elements per feature in the batch (N*H*W, or N for BN1d)       */
   int train;                 /* 1: batch statistics, 0: running statistics (eval mode)         */
   float eps;
+  /* Finalised constants (train mode; optional).  A launch of the specialised GEMM core that produces
+   * this layer's forward sums (CV_STAT_FWD epilogue with this layer as ebn) elects its last workgroup
+   * with ticket[0] and writes cfwd = [sc][mu][beta][istd] (4*C floats, sc = gamma*istd); one that
+   * produces the backward sums (CV_STAT_BWD epilogue) uses ticket[1] and writes
+   * cbwd = [sc][c1][mu][istd][c2] (5*C floats, c1 = sum dz / n, c2 = sum dz*xhat / n).  A consuming
+   * GEMM uses cfwd / cbwd only when the matching ticket is non-zero (its producer finalised) and
+   * otherwise folds the replica sums itself; every other producer leaves the ticket at zero.  Both
+   * tickets must be zero before the producing launch (they live in the zeroed statistics arena). */
+  float* cfwd;
+  float* cbwd;
+  unsigned int* ticket;      /* [2] */
 } cv_bn;
 
 /* transform applied while an operand is staged into LDS */
@@ -73,7 +86,8 @@ typedef struct cv_epilogue {
   double* stat_out;   /* [REPL][2][C]                                               */
   int stat_div;       /* feature index = column / stat_div (1 = per column)         */
   const float* ey;    /* STAT_BWD: pre-BN values at the output positions            */
-  cv_bn ebn;          /* STAT_BWD: the BN layer (batch statistics)                  */
+  cv_bn ebn;          /* the BN layer fed by this output: STAT_BWD needs its batch statistics;
+                         with ebn.ticket set (either mode) the producer finalises its constants */
   int erelu;          /* STAT_BWD: 1 if ReLU follows that BN                        */
 } cv_epilogue;
 
