@@ -204,8 +204,8 @@ _SIGS = {
     ),
     "cv_mi_learning_step": (
         c_int,
-        [_P(cv_mlp), c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, _P(cv_mlp_grad), c_void_p, c_void_p,
-         c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
+        [_P(cv_mlp), c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, _P(cv_mlp_grad), c_void_p,
+         c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
     ),
     "cv_adam_step": (
         c_int,

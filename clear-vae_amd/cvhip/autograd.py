@@ -367,8 +367,10 @@ class LearningLossFn(torch.autograd.Function):
         gb = [torch.empty_like(p) for p in ps]
         G = cv_mlp_grad(*[t.data_ptr() for t in gb])
         out = torch.empty((), dtype=torch.float32, device=xx.device)
+        work = torch.zeros(int(_lib.lib().cv_mi_workspace_bytes(n)) // 4 + 16, dtype=torch.float32,
+                           device=xx.device)
         _lib.call("cv_mi_learning_step", mlp, xx.data_ptr(), xx.stride(0), yy.data_ptr(), yy.stride(0), n,
-                  out.data_ptr(), G, None, None, None, None, 0, None, None, _lib.stream_handle())
+                  work.data_ptr(), out.data_ptr(), G, None, None, None, None, 0, None, None, _lib.stream_handle())
         ctx.gb = gb
         ctx.xy_grad = (x.requires_grad, y.requires_grad)
         return out

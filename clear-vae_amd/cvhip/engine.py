@@ -307,7 +307,7 @@ class ClearStep:
                     ws.reparam_program(lp, eps_buf[1 + j] if inject else None, self.seed, self.offset)
                     ws.decoder_program(lp, ws.z, True, "none")
                     ws.running_program(lp, "all")
-                    lp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n,
+                    lp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
                            self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
                            E.numel, self.est_adam.hyper, self.est_adam.step)
                 return lp
@@ -325,7 +325,7 @@ class ClearStep:
                     ws.reparam_program(gp, eps_buf[1 + j] if inject else None, self.seed, self.offset)
                     ws.decoder_program(gp, ws.z, True, "none")
                     ws.running_program(gp, "all")
-                    gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n,
+                    gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
                            self.learn.data_ptr() + 4 * j, G, None, None, None, None, 0, None, None)
                     ap = Program()
                     ap.add("cv_adam_step", E.flat, E.grad, self.est_adam.m, self.est_adam.v, E.numel,

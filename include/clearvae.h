@@ -277,9 +277,12 @@ int cv_mi_backward(int kind, const cv_mlp* mlp, const float* x, int ldx, const f
                    const float* z, float* dheads, int d, cv_stream_t stream);
 /* learning_loss = -loglikeli (mi_estimator.py:129-131, 193-198): loss and MLP gradients
  * (overwritten); with params != NULL also the Adam update of the estimator arena
- * (trainer.py:885-887). */
+ * (trainer.py:885-887), whose grads arena must then hold g's buffers.  `work`: a
+ * cv_mi_workspace_bytes(n) buffer, zeroed once at allocation (its arrival counters reset
+ * themselves). */
 int cv_mi_learning_step(const cv_mlp* mlp, const float* x, int ldx, const float* y, int ldy, int n,
-                        float* loss_out, const cv_mlp_grad* g, float* params, const float* grads,
+                        void* work, float* loss_out, const cv_mlp_grad* g, float* params,
+                        const float* grads,
                         float* exp_avg, float* exp_avg_sq, int64_t numel, const float* hyper,
                         int64_t* step, cv_stream_t stream);
 
