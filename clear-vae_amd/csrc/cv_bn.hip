@@ -390,9 +390,48 @@ __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int 
   }
 }
 
+// ---------------------------------------------------------------- multi-buffer zero
+struct ZeroArgs {
+  uint32_t* p[8];
+  long words[8];
+  long start[9];  // prefix sums of words
+  int count;
+};
+
+__global__ __launch_bounds__(256) void zero_many_kernel(const ZeroArgs z) {
+  const long total = z.start[z.count];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int b = 0;
+#pragma unroll
+    for (int q = 1; q < 8; ++q)
+      if (q < z.count && i >= z.start[q]) b = q;
+    z.p[b][i - z.start[b]] = 0u;
+  }
+}
+
 }  // namespace cv
 
 using namespace cv;
+
+extern "C" int cv_zero_many(void* const* ptrs, const size_t* bytes, int count, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(ptrs && bytes && count > 0 && count <= 8, "zero_many: 1..8 buffers");
+  ZeroArgs z;
+  memset(&z, 0, sizeof(z));
+  z.count = count;
+  for (int i = 0; i < count; ++i) {
+    CV_REQUIRE(ptrs[i] && bytes[i] % 4 == 0 && (uintptr_t)ptrs[i] % 4 == 0, "zero_many: buffer %d not 4-byte granular", i);
+    z.p[i] = (uint32_t*)ptrs[i];
+    z.words[i] = (long)(bytes[i] / 4);
+    z.start[i + 1] = z.start[i] + z.words[i];
+  }
+  long g = (z.start[count] + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(zero_many_kernel, dim3((int)g), dim3(256), 0, S(stream), z);
+  CV_LAUNCH_CHECK("zero_many");
+  return 0;
+}
 
 extern "C" int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum, int64_t* const* nbt,
                                     cv_stream_t stream) {

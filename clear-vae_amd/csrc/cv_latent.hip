@@ -10,7 +10,7 @@
 namespace cv {
 
 // ---------------------------------------------------------------- reparameterisation
-// One workgroup; offset[0] is read by every thread and advanced by thread 0 after a barrier.
+// offset[0] is read by every thread; the last workgroup to arrive (counted in offset[1]) advances it.
 __global__ __launch_bounds__(256) void reparam_kernel(const float* __restrict__ heads, int n, int d,
                                                        const float* __restrict__ eps_in, uint64_t seed,
                                                        uint64_t* offset, float* __restrict__ z,
@@ -34,6 +34,16 @@ __global__ __launch_bounds__(256) void reparam_kernel(const float* __restrict__ 
       const float sd = expf(0.5f * lv);
       z[e] = mu + ep * sd;
       if (eps_out) eps_out[e] = ep;
+    }
+  }
+  if (offset && !eps_in) {  // the last workgroup to finish advances the counter (offset[1]: arrivals)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long prev = atomicAdd((unsigned long long*)(offset + 1), 1ull);
+      if (prev == (unsigned long long)(gridDim.x - 1)) {
+        offset[0] = off + 1;
+        offset[1] = 0;
+      }
     }
   }
 }
@@ -461,10 +471,293 @@ __global__ __launch_bounds__(256) void ntxent_grad_kernel(const NtArgs A) {
   }
 }
 
+// ---------------------------------------------------------------- NT-Xent, LDS-staged
+// The latent heads are row-major [n][4d] (mu_c, lv_c, mu_s, lv_s): a lane walking its own column j
+// reads d words 16d bytes apart, so every global load instruction of the kernels above touches 64
+// cache lines.  These variants stage the branch's mu / logvar rows once per workgroup in LDS with an
+// odd row pitch (d+1: lanes on consecutive rows hit distinct banks), together with the labels, the
+// row norms and (backward) the row log-sum-exps, and give each workgroup NTL_ROWS rows.
+constexpr int NTL_ROWS = 4;  // rows per 256-thread workgroup (one per wave)
+
+struct NtLds {
+  float* mu;   // [n][d+1]
+  float* lv;   // [n][d+1] (similarities that use logvar)
+  float* nrm;  // [n] clamped norms (cosine)
+  float* raw;  // [n] raw norms (cosine, backward)
+  float* lse;  // [2n] (backward)
+  long long* lab;
+};
+
+static size_t ntl_bytes(int n, int d, bool need_lv, bool grad) {
+  const size_t pd = (size_t)d + 1;
+  return (size_t)n * 8 + (size_t)n * pd * 4 * (need_lv ? 2 : 1) + (size_t)n * 4 * (grad ? 4 : 1);
+}
+
+__device__ __forceinline__ NtLds ntl_carve(char* s, int n, int d, bool need_lv, bool grad) {
+  NtLds L;
+  const int pd = d + 1;
+  L.lab = (long long*)s;
+  float* p = (float*)(s + (size_t)n * 8);
+  L.mu = p;
+  p += (size_t)n * pd;
+  L.lv = nullptr;
+  if (need_lv) {
+    L.lv = p;
+    p += (size_t)n * pd;
+  }
+  L.nrm = p;
+  p += n;
+  L.raw = grad ? p : nullptr;
+  if (grad) p += n;
+  L.lse = grad ? p : nullptr;
+  return L;
+}
+
+__device__ __forceinline__ void ntl_stage(const Branch& b, const int64_t* label, int n, int d, bool need_lv,
+                                          bool cosine, bool grad, NtLds& L) {
+  const int t = threadIdx.x, pd = d + 1;
+  const FDiv fd = FDiv::make(d);
+  // batches of 8 loads in flight per thread before the LDS writes (one latency per batch)
+  constexpr int U = 8;
+  const int nd = n * d;
+  for (int base = t; base < nd; base += 256 * U) {
+    float vm[U], vl[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = base + q * 256;
+      const int r = fd.div(i), k = i - r * d;
+      vm[q] = (i < nd) ? b.mu[(size_t)r * b.ld + k] : 0.f;
+      vl[q] = (need_lv && i < nd) ? b.lv[(size_t)r * b.ld + k] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = base + q * 256;
+      const int r = fd.div(i), k = i - r * d;
+      if (i < nd) {
+        L.mu[r * pd + k] = vm[q];
+        if (need_lv) L.lv[r * pd + k] = vl[q];
+      }
+    }
+  }
+  for (int base = t; base < n; base += 256 * U) {
+    long long lb[U];
+    float la[U], lp[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = base + q * 256;
+      lb[q] = (i < n) ? label[i] : 0;
+      la[q] = (grad && i < n) ? b.lse[i] : 0.f;
+      lp[q] = (grad && i < n) ? b.lse[n + i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = base + q * 256;
+      if (i < n) {
+        L.lab[i] = lb[q];
+        if (grad) {
+          L.lse[i] = la[q];
+          L.lse[n + i] = lp[q];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (cosine) {
+    for (int j = t; j < n; j += 256) {
+      float s = 0.f;
+      for (int k = 0; k < d; ++k) {
+        const float v = L.mu[j * pd + k];
+        s += v * v;
+      }
+      const float r = sqrtf(s);
+      L.nrm[j] = fmaxf(r, 1e-8f);
+      if (grad) L.raw[j] = r;
+    }
+    __syncthreads();
+    // cosine: rows become the unit vectors u_j = mu_j / max(|mu_j|, 1e-8) (the very quotients the
+    // pair loops would otherwise recompute per pair)
+    for (int i = t; i < nd; i += 256) {
+      const int r = fd.div(i), k = i - r * d;
+      L.mu[r * pd + k] = L.mu[r * pd + k] / L.nrm[r];
+    }
+  }
+  __syncthreads();
+}
+
+template <int DM>
+__device__ __forceinline__ float dot_u(const float* a, const float* b, int d) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) s += b[k] * a[k];
+  return s;
+}
+
+template <int DM>
+__device__ __forceinline__ void ntl_theta(const NtLds& L, int r, int d, float* m, float* l, bool need_lv) {
+  const int pd = d + 1;
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    m[k] = (k < d) ? L.mu[r * pd + k] : 0.f;
+    l[k] = (need_lv && k < d) ? L.lv[r * pd + k] : 0.f;
+  }
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void ntxent_rows_lds_kernel(const NtArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char ntl_smem[];
+  const Branch& b = A.br[blockIdx.y];
+  const int n = A.n, d = A.d;
+  const bool cosine = A.sim == CV_SIM_COSINE;
+  const bool need_lv = !(A.sim == CV_SIM_COSINE || A.sim == CV_SIM_L2);
+  NtLds L = ntl_carve(ntl_smem, n, d, need_lv, false);
+  ntl_stage(b, A.label, n, d, need_lv, cosine, false, L);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int iend = min(n, (int)(blockIdx.x + 1) * NTL_ROWS);
+  for (int i = blockIdx.x * NTL_ROWS + w; i < iend; i += 4) {
+    float mi[DM], li[DM], mj[DM], lj[DM];
+    ntl_theta<DM>(L, i, d, mi, li, need_lv);
+    const long long lab = L.lab[i];
+    float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
+    for (int j = lane; j < n; j += 64) {
+      if (j == i) continue;
+      ntl_theta<DM>(L, j, d, mj, lj, need_lv);
+      const float S = cosine ? dot_u<DM>(mi, mj, d) : sim_ij<DM>(A.sim, mi, li, 1.f, mj, lj, 1.f, d);
+      const float s = S / A.tau;
+      lse_merge(ma, sa, s, 1.f);
+      const bool pos = b.ps ? (L.lab[j] != lab) : (L.lab[j] == lab);
+      if (pos) lse_merge(mp, sp, s, 1.f);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(ma, o, 64), s2 = __shfl_xor(sa, o, 64);
+      const float m3 = __shfl_xor(mp, o, 64), s3 = __shfl_xor(sp, o, 64);
+      lse_merge(ma, sa, m2, s2);
+      lse_merge(mp, sp, m3, s3);
+    }
+    if (lane == 0) {
+      b.lse[i] = (sa > 0.f) ? ma + logf(sa) : -INFINITY;
+      b.lse[n + i] = (sp > 0.f) ? mp + logf(sp) : -INFINITY;
+    }
+  }
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void ntxent_grad_lds_kernel(const NtArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char ntl_smem[];
+  __shared__ float scratch[16];
+  __shared__ double dscratch[16];
+  const Branch& b = A.br[blockIdx.y];
+  const int n = A.n, d = A.d;
+  const bool cosine = A.sim == CV_SIM_COSINE;
+  const bool need_lv = !(A.sim == CV_SIM_COSINE || A.sim == CV_SIM_L2);
+  NtLds L = ntl_carve(ntl_smem, n, d, need_lv, true);
+  ntl_stage(b, A.label, n, d, need_lv, cosine, true, L);
+  // finite-row count (and, in block 0, the loss)
+  float cnt = 0.f;
+  double lsum = 0.0;
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const float l = L.lse[j] - L.lse[n + j];
+    if (isfinite(l)) {
+      cnt += 1.f;
+      lsum += (double)l;
+    }
+  }
+  const float nf = block_sum<256>(cnt, scratch);
+  if (blockIdx.x == 0) {
+    const double tot = block_sum<256>(lsum, dscratch);
+    if (threadIdx.x == 0 && b.loss_out) b.loss_out[0] = (nf > 0.f) ? (float)(tot / (double)nf) : NAN;
+  }
+  if (!b.dmu) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float gup = b.gmul * (b.gscale ? b.gscale[0] : 1.0f);
+  const float c = (nf > 0.f) ? gup / (nf * A.tau) : 0.f;
+  const int iend = min(n, (int)(blockIdx.x + 1) * NTL_ROWS);
+  for (int i = blockIdx.x * NTL_ROWS + w; i < iend; i += 4) {
+    float mi[DM], li[DM], mj[DM], lj[DM], gm[DM], gl[DM];
+    ntl_theta<DM>(L, i, d, mi, li, need_lv);
+#pragma unroll
+    for (int k = 0; k < DM; ++k) { gm[k] = 0.f; gl[k] = 0.f; }
+    const float ni = cosine ? L.nrm[i] : 1.f;
+    const bool clamped_i = cosine && !(L.raw[i] > 1e-8f);
+    const long long lab = L.lab[i];
+    const float la_i = L.lse[i], lp_i = L.lse[n + i];
+    const bool fin_i = isfinite(la_i - lp_i);
+    for (int j = lane; j < n; j += 64) {
+      if (j == i) continue;
+      ntl_theta<DM>(L, j, d, mj, lj, need_lv);
+      const float S = cosine ? dot_u<DM>(mi, mj, d) : sim_ij<DM>(A.sim, mi, li, 1.f, mj, lj, 1.f, d);
+      const float s = S / A.tau;
+      const bool pos = b.ps ? (L.lab[j] != lab) : (L.lab[j] == lab);
+      const float la_j = L.lse[j], lp_j = L.lse[n + j];
+      const bool fin_j = isfinite(la_j - lp_j);
+      float G = 0.f;
+      if (fin_i) G += c * (expf(s - la_i) - (pos ? expf(s - lp_i) : 0.f));
+      if (fin_j) G += c * (expf(s - la_j) - (pos ? expf(s - lp_j) : 0.f));
+      if (G != 0.f) {
+        if (cosine) {  // d S / d mu_i = (u_j - S u_i) / n_i (u_j when |mu_i| is clamped); 1/n_i applied once below
+#pragma unroll
+          for (int k = 0; k < DM; ++k)
+            if (k < d) gm[k] += G * (clamped_i ? mj[k] : (mj[k] - S * mi[k]));
+        } else {
+          sim_grad_row<DM>(A.sim, mi, li, 1.f, false, mj, lj, 1.f, S, G, d, gm, gl);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DM; ++k) {
+      if (k < d) {
+        gm[k] = wave_sum(gm[k]);
+        if (cosine) gm[k] = gm[k] / ni;
+        if (need_lv) gl[k] = wave_sum(gl[k]);
+      }
+    }
+    // lane k writes component k (a coalesced row store instead of d scalar stores from lane 0)
+    float om = 0.f, ol = 0.f;
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k == lane) { om = gm[k]; ol = need_lv ? gl[k] : 0.f; }
+    if (lane < d) {
+      float* pm = b.dmu + (size_t)i * b.gld + lane;
+      *pm = A.accumulate ? *pm + om : om;
+      if (b.dlv) {
+        float* pl = b.dlv + (size_t)i * b.gld + lane;
+        *pl = A.accumulate ? *pl + ol : ol;
+      }
+    }
+  }
+}
+
 template <template <int> class K>
 struct DDispatch;
 
+// LDS-staged variants when the branch fits (the common case); the global-walk kernels otherwise
+static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st) {
+  const bool need_lv = !(a.sim == CV_SIM_COSINE || a.sim == CV_SIM_L2);
+  const size_t lds = ntl_bytes(a.n, a.d, need_lv, !rows);
+  if (lds > 144 * 1024) return -1;
+  const dim3 grid(cdiv(a.n, NTL_ROWS), nbr);
+  const void* kern;
+  if (a.d <= 8) kern = rows ? (const void*)ntxent_rows_lds_kernel<8> : (const void*)ntxent_grad_lds_kernel<8>;
+  else if (a.d <= 16) kern = rows ? (const void*)ntxent_rows_lds_kernel<16> : (const void*)ntxent_grad_lds_kernel<16>;
+  else if (a.d <= 32) kern = rows ? (const void*)ntxent_rows_lds_kernel<32> : (const void*)ntxent_grad_lds_kernel<32>;
+  else kern = rows ? (const void*)ntxent_rows_lds_kernel<64> : (const void*)ntxent_grad_lds_kernel<64>;
+  if (lds > 64 * 1024 && hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  NtArgs arg = a;
+  void* params[] = {&arg};
+  if (hipLaunchKernel(kern, grid, dim3(256), params, lds, st) != hipSuccess) {
+    ::cv::set_error("%s: launch failed", rows ? "ntxent_rows" : "ntxent_grad");
+    return 2;
+  }
+  return 0;
+}
+
 static int ntxent_launch(const NtArgs& a, int nbr, bool rows, hipStream_t st) {
+  const int r = ntxent_launch_lds(a, nbr, rows, st);
+  if (r >= 0) return r;
   dim3 grid(cdiv(a.n, NT_ROWS), nbr);
   if (a.d <= 8) {
     if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<8>, grid, dim3(256), 0, st, a);
@@ -498,7 +791,7 @@ extern "C" int cv_reparam_forward(const float* heads, int n, int d, const float*
   hipLaunchKernelGGL(reparam_kernel, dim3((int)blocks), dim3(256), 0, S(stream), heads, n, d, eps, seed, offset, z,
                      eps_out);
   CV_LAUNCH_CHECK("reparam_forward");
-  if (offset) {  // the Philox offset moves once per call, after every block has read it
+  if (offset && eps) {  // injected noise: the counter still moves once per call
     hipLaunchKernelGGL(offset_advance_kernel, dim3(1), dim3(1), 0, S(stream), offset);
     CV_LAUNCH_CHECK("reparam_offset");
   }

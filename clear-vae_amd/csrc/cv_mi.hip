@@ -640,13 +640,14 @@ __global__ __launch_bounds__(256) void mi_learn_reduce_kernel(const LearnArgs A,
 
 // ---------------------------------------------------------------- Adam over a flat arena
 // torch.optim.Adam (foreach) over a flat arena: grid-stride float4 (the arena is 16-byte aligned and
-// padded to a multiple of 4), bias corrections computed once per block.  The step counters are
-// advanced by adam_advance_kernel right after (a one-thread launch, so no block has to detect being
-// the last one through a contended atomic).
+// padded to a multiple of 4), bias corrections computed once per block.  The last workgroup to
+// arrive (arrivals counted in step[1]) advances the step counters.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ gr,
                                                    float* __restrict__ m, float* __restrict__ v, long numel,
-                                                   const float* hyper, const int64_t* step, const float* gscale) {
+                                                   const float* hyper, int64_t* step, const float* gscale,
+                                                   int64_t* aux) {
   __shared__ float cst[8];
+  __shared__ int flag;
   if (threadIdx.x == 0) {
     const long t_step = step[0] + 1;
     const double b1 = hyper[1], b2 = hyper[2];
@@ -692,12 +693,18 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     m[i] = mm;
     v[i] = vv;
   }
-}
-
-__global__ void adam_advance_kernel(int64_t* step, int64_t* aux) {
-  step[0] += 1;
-  step[1] = 0;
-  if (aux) aux[0] += 1;
+  // every workgroup read step[0] (thread 0, before the first barrier) before taking its ticket
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long prev = atomicAdd((unsigned long long*)(step + 1), 1ull);
+    flag = prev == (unsigned long long)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (flag && threadIdx.x == 0) {
+    step[0] += 1;
+    step[1] = 0;
+    if (aux) aux[0] += 1;
+  }
 }
 
 }  // namespace cv
@@ -839,9 +846,7 @@ extern "C" int cv_adam_step(float* params, const float* grads, float* exp_avg, f
   if (g > 512) g = 512;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(g), dim3(256), 0, S(stream), params, grads, exp_avg, exp_avg_sq, (long)numel,
-                     hyper, step, grad_scale);
+                     hyper, step, grad_scale, aux_counter);
   CV_LAUNCH_CHECK("adam_step");
-  hipLaunchKernelGGL(adam_advance_kernel, dim3(1), dim3(1), 0, S(stream), step, aux_counter);
-  CV_LAUNCH_CHECK("adam_advance");
   return 0;
 }

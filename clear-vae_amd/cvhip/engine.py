@@ -40,7 +40,7 @@ from . import _lib, rng
 from . import dist as cvdist
 from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
 from .autograd import est_params, mlp_struct
-from .plan import ParamArena, Program, Workspace, ensure_arena, pack_program
+from .plan import ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
 
 
 def _dist_world():
@@ -243,10 +243,14 @@ class ClearStep:
 
         def make_fwd(inject: bool):
             f = Program()
-            f.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-            f.add("cv_zero", A.grad, A.numel * 4)
+            # one launch zeroes the BN sums, the gradient arena and the two split-K / accumulated
+            # latent buffers of the step
+            bufs = [(ws.stats, ws.stats.numel() * 8), (A.grad, A.numel * 4), (ws.heads, ws.heads.numel() * 4),
+                    (ws.dz, ws.dz.numel() * 4)]
+            f.add("cv_zero_many", ptr_array([b.data_ptr() for b, _ in bufs]),
+                  (ctypes.c_size_t * len(bufs))(*[nb for _, nb in bufs]), len(bufs))
             pack_program(sp, f, "all")
-            ws.encoder_program(f, X, True)
+            ws.encoder_program(f, X, True, zero_heads=False)
             ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
             ws.decoder_program(f, ws.z, True, "loss", X)
             ws.running_program(f, "all")
@@ -255,7 +259,7 @@ class ClearStep:
         fwd, fwd_inj = make_fwd(False), make_fwd(True)
         # decoder backward (bucket 1 of the gradient arena)
         dec = Program()
-        ws.decoder_backward_program(dec, pg, ws.dz)
+        ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False)
         ws.bn_grads_program(dec, pg, "dec")
         # latent terms -> d(heads)
         lat = Program()

@@ -480,7 +480,7 @@ class Workspace:
             self.running_program(P, "all")
         return P
 
-    def encoder_program(self, P: Program, x, train: bool):
+    def encoder_program(self, P: Program, x, train: bool, zero_heads: bool = True):
         sp, n = self.spec, self.n
         cur = None
         for li, c in enumerate(sp.enc):
@@ -495,7 +495,8 @@ class Workspace:
         # heads (Linear on the NCHW-flattened activation), split-K into a zeroed buffer
         C, Hh, Wh = sp.feat
         lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
-        P.add("cv_zero", self.heads, self.heads.numel() * 4)
+        if zero_heads:  # (else the caller zeroed it earlier in the same program)
+            P.add("cv_zero", self.heads, self.heads.numel() * 4)
         P.add("cv_linear_forward", lin, operand(cur, XF_BNRELU, self.bn_enc[-1].cv(train)),
               sp.heads[0].weight.data_ptr(), sp.heads[0].bias.data_ptr(), self.heads, 1, ep_none())
 
@@ -532,7 +533,7 @@ class Workspace:
             P.add("cv_output_loss", self.bn_dec[-1].cv(True), cur, x, n, sp.in_ch, hw, self.xhat,
                   self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
 
-    def decoder_backward_program(self, P: Program, param_grad, dz_out):
+    def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True):
         """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to
         dz_out [n, 2d] (zeroed + accumulated) and the decoder parameter gradients."""
         sp, n = self.spec, self.n
@@ -554,7 +555,8 @@ class Workspace:
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
         P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
               self.z, param_grad(sp.dec_lin.weight))
-        P.add("cv_zero", dz_out, dz_out.numel() * 4)
+        if zero_dz:  # (else the caller zeroed it earlier in the step)
+            P.add("cv_zero", dz_out, dz_out.numel() * 4)
         gout = operand(self.gah, XF_BNBWD, self.bn_1d.cv(True), y=self.h)
         P.add("cv_linear_backward_data", lin, gout, sp.dec_lin.weight, dz_out, 1, ep_none())
 

@@ -193,7 +193,8 @@ int cv_output_backward(const cv_bn* bn, const float* y, const float* xhat, const
 /* ---- reparameterisation (vae.py:56-79) ---- */
 /* heads: [n][4d] = (mu_c | logvar_c | mu_s | logvar_s); z: [n][2d] = (z_c | z_s).
  * eps == NULL: eps ~ N(0,1) from a counter-based Philox4x32-10 stream keyed by (seed, offset[0]);
- * offset is a device uint64 advanced by the kernel (graph-replay safe).  eps != NULL: [n][2d]
+ * offset is a device uint64[2] (counter, zeroed arrival word) advanced by the kernel (graph-replay
+ * safe).  eps != NULL: [n][2d]
  * injected noise (test hook).  eps_out (optional) receives the noise used. */
 int cv_reparam_forward(const float* heads, int n, int d, const float* eps, uint64_t seed,
                        uint64_t* offset, float* z, float* eps_out, cv_stream_t stream);
@@ -303,6 +304,8 @@ int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dgamma, float*
 /* ---- misc ---- */
 /* hipMemsetAsync(ptr, 0, bytes, stream) (graph-capturable) */
 int cv_zero(void* ptr, size_t bytes, cv_stream_t stream);
+/* zero up to 8 buffers (4-byte granular: sizes multiples of 4, 4-byte aligned) in one launch */
+int cv_zero_many(void* const* ptrs, const size_t* bytes, int count, cv_stream_t stream);
 const char* cv_last_error(void);
 int cv_version(void);
 /* test hook: 1 routes every conv/linear GEMM to the generic implicit-GEMM kernel instead of the
