@@ -68,6 +68,15 @@ int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const flo
                   const cv_epilogue* ep, hipStream_t st);
 int narrow_scatter(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
                    const cv_epilogue* ep, hipStream_t st);
+// LDS-banded kernels for the image-side convs (<= 4 big-grid channels, 32 small-grid channels;
+// cv_edge.hip); -1 when the geometry is not one they serve
+int edge_gather(const Geo& g, const cv_operand* in, const float* wg, const float* bias, float* out,
+                const cv_epilogue* ep, hipStream_t st);
+int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
+                 const cv_epilogue* ep, hipStream_t st);
+int edge_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias, float* work,
+               size_t work_bytes, hipStream_t st);
+size_t edge_wgrad_ws_bytes(const Geo& g, bool bias);
 
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
@@ -251,11 +260,19 @@ __device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, boo
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    // two-level arrival count: <= 64 groups of gsz consecutive workgroups; the last of a group
+    // arrives at ticket[dir], the last group elects the finalising workgroup
     const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
-    const unsigned prev =
-        __hip_atomic_fetch_add(b.ticket + (bwd ? 1 : 0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (prev == nblk - 1) ? 1 : 0;
-    if (prev == nblk - 1) {  // acquire once, before the barrier that publishes the flag to the block
+    const unsigned me = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned gsz = (nblk + 63) / 64, ngrp = (nblk + gsz - 1) / gsz, grp = me / gsz;
+    const unsigned gcnt = (grp + 1 == ngrp) ? nblk - grp * gsz : gsz;
+    unsigned* gctr = b.ticket + 2 + (bwd ? 64 : 0) + grp;
+    bool last = false;
+    if (__hip_atomic_fetch_add(gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gcnt - 1)
+      last = __hip_atomic_fetch_add(b.ticket + (bwd ? 1 : 0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             ngrp - 1;
+    *flag = last ? 1 : 0;
+    if (last) {  // acquire once, before the barrier that publishes the flag to the block
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

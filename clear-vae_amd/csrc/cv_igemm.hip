@@ -893,6 +893,10 @@ static int check_conv(const cv_conv* g) {
 // GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
 static int run_gather(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                       const cv_epilogue* ep, hipStream_t st, const char* what) {
+  if (!g_force_generic) {
+    const int er = edge_gather(g, in, w, bias, out, ep, st);
+    if (er >= 0) return er;
+  }
   const int nr = narrow_gather(g, in, w, bias, out, ep, st);
   if (nr >= 0) return nr;
   Args a;
@@ -918,6 +922,10 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
 // SCATTER with big = rows. `in` is the small-grid tensor; w is packed [tap][cs][cb].
 static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                        const cv_epilogue* ep, hipStream_t st, const char* what) {
+  if (!g_force_generic) {
+    const int er = edge_scatter(g, in, w, bias, out, ep, st);
+    if (er >= 0) return er;
+  }
   const int nr = narrow_scatter(g, in, w, bias, out, ep, st);
   if (nr >= 0) return nr;
   Args a;
@@ -987,8 +995,17 @@ static int launch_wgrad_reduce(const float* part, int split, int M, int N, int n
   return 0;
 }
 
+int wgrad_reduce_launch(const float* part, int split, int M, int N, int ntot, int cb, int kk, float* gw,
+                        float* gbias, hipStream_t st) {
+  return launch_wgrad_reduce(part, split, M, N, ntot, cb, kk, gw, gbias, st);
+}
+
 static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias,
                      int split_k, float* work, size_t work_bytes, hipStream_t st) {
+  if (split_k <= 0 && !g_force_generic) {
+    const int er = edge_wgrad(g, small, big, gw, gbias, work, work_bytes, st);
+    if (er >= 0) return er;
+  }
   Args a;
   init_args(a);
   a.op = OP_WGRAD;
@@ -1083,7 +1100,9 @@ extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, c
 extern "C" size_t cv_conv_wgrad_workspace_bytes(const cv_conv* g, int split_k) {
   if (!g) return 0;
   const Geo geo = geo_of(g);
-  return wgrad_ws_bytes(geo.cs, geo.kh * geo.kw * geo.cb, (long)geo.n * geo.hs * geo.ws, split_k);
+  const size_t gen = wgrad_ws_bytes(geo.cs, geo.kh * geo.kw * geo.cb, (long)geo.n * geo.hs * geo.ws, split_k);
+  const size_t edge = split_k > 0 ? 0 : edge_wgrad_ws_bytes(geo, true);
+  return gen > edge ? gen : edge;
 }
 
 extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, const cv_operand* gout,

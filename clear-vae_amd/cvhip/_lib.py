@@ -21,6 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CVHIP_LIB") or os.path.join(_HERE, "libclearvae_hip.so")
 
 REC_REPL = 32  # CV_REC_REPL
+TICKET_WORDS = 130  # CV_TICKET_WORDS
 
 
 def stat_repl(C: int) -> int:

@@ -413,8 +413,9 @@ class Workspace:
         # fp64 statistics arena: per BN layer [REPL,2,C] forward + [REPL,2,C] backward, plus scalars
         bns = spec.bn_layers
         counts = [n * c.h_out * c.w_out for c in spec.enc] + [n] + [n * c.h_out * c.w_out for c in spec.dec]
-        # (+ one 8-byte ticket pair per layer after the scalars: zeroed with the statistics)
-        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 64 + len(bns)
+        # (+ CV_TICKET_WORDS arrival counters per layer after the scalars: zeroed with the statistics)
+        tw = (_lib.TICKET_WORDS + 1) // 2  # in 8-byte words
+        tot = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns) + 64 + tw * len(bns)
         self.stats = torch.zeros(tot, dtype=torch.float64, device=device)
         # finalised BN constants (written by each layer's producing launch, read by the GEMM prologues)
         r4 = lambda v: (v + 3) & ~3  # noqa: E731  (16-byte aligned slots)
@@ -435,7 +436,7 @@ class Workspace:
             bv.cfwd = self.bn_consts[oc:oc + 4 * C]
             bv.cbwd = self.bn_consts[oc + r4(4 * C):oc + r4(4 * C) + 5 * C]
             oc += r4(4 * C) + r4(5 * C)
-            bv.ticket = self.stats.data_ptr() + 8 * (o + 64 + i)
+            bv.ticket = self.stats.data_ptr() + 8 * (o + 64 + tw * i)
         # interior layers: produced and consumed by GEMM-core launches in both directions (the layers
         # next to the image-facing convs and the BatchNorm1d are served by the narrow / BN kernels)
         self.bn_enc = self.bnv[: len(spec.enc)]
@@ -443,9 +444,11 @@ class Workspace:
         self.bn_dec = self.bnv[len(spec.enc) + 1:]
         nd = len(spec.dec)
         for i, bv in enumerate(self.bn_enc):
-            bv.fin_fwd = bv.fin_bwd = i >= 1 and bv.C % 32 == 0
+            bv.fin_fwd = i >= 1 and bv.C % 32 == 0
+            bv.fin_bwd = bv.C % 32 == 0  # (layer 0: produced by a GEMM-core bwd-data, read by the edge wgrad)
         for j, bv in enumerate(self.bn_dec):
-            bv.fin_fwd = bv.fin_bwd = j + 2 < nd and bv.C % 32 == 0
+            bv.fin_fwd = j + 1 < nd and bv.C % 32 == 0  # (layer nd-2: read by the edge scatter / wgrad)
+            bv.fin_bwd = j + 2 < nd and bv.C % 32 == 0
         self.rec = self.scal[0:_lib.REC_REPL]
         if with_grad:
             self.g_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]

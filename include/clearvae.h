@@ -36,6 +36,7 @@ typedef void* cv_stream_t; /* a hipStream_t (torch.cuda.current_stream().cuda_st
  * atomics of thousands of producer workgroups do not serialise on a few addresses. */
 #define CV_REC_REPL 32
 #define CV_STAT_REPL(C) ((C) >= 256 ? 8 : (C) >= 64 ? 16 : 32)
+#define CV_TICKET_WORDS 130
 
 /* ---- BatchNorm as seen by a fused prologue/epilogue (nn.BatchNorm1d/2d, vae.py:17-44, 115-154) ---- */
 typedef struct cv_bn {
@@ -55,11 +56,14 @@ typedef struct cv_bn {
    * produces the backward sums (CV_STAT_BWD epilogue) uses ticket[1] and writes
    * cbwd = [sc][c1][mu][istd][c2] (5*C floats, c1 = sum dz / n, c2 = sum dz*xhat / n).  A consuming
    * GEMM uses cfwd / cbwd only when the matching ticket is non-zero (its producer finalised) and
-   * otherwise folds the replica sums itself; every other producer leaves the ticket at zero.  Both
-   * tickets must be zero before the producing launch (they live in the zeroed statistics arena). */
+   * otherwise folds the replica sums itself; every other producer leaves the ticket at zero.  The
+   * arrivals are counted in two levels (<= 64 groups of workgroups, CV_TICKET_WORDS words:
+   * ticket[0..1] = groups done, then 64 group counters per direction) so thousands of workgroups do
+   * not serialise on one address.  All words must be zero before the producing launch (they live in
+   * the zeroed statistics arena). */
   float* cfwd;
   float* cbwd;
-  unsigned int* ticket;      /* [2] */
+  unsigned int* ticket;      /* [CV_TICKET_WORDS] */
 } cv_bn;
 
 /* transform applied while an operand is staged into LDS */
