@@ -89,7 +89,7 @@ def kernel_pass(engine, G, reps=20, rounds=3):
         progs.append(("learn", learn))
     times = {}
     for pname, P in progs:
-        for i, (name, fn, args) in enumerate(P.calls):
+        for i, (name, fn, args, _lane) in enumerate(P.calls):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 s = _lib.stream_handle()
@@ -118,7 +118,7 @@ def gemm_flops_of(label, G, engine):
     idx = int(rest.split("]")[0])
     if not hasattr(G.get(pname), "calls"):
         return None
-    name, fn, args = G[pname].calls[idx]
+    name, fn, args, _lane = G[pname].calls[idx]
     if name.startswith("cv_conv_"):
         g = args[0]._obj
         k = g.kh * g.kw
@@ -259,7 +259,7 @@ def main():
 
         G = eng.graphs[B]
         pname, idx = args.only_call.split("[")
-        name, fn, cargs = G[pname].calls[int(idx.rstrip("]"))]
+        name, fn, cargs, _lane = G[pname].calls[int(idx.rstrip("]"))]
         s_ = _lib.stream_handle()
         for _ in range(args.reps):
             _lib.check(fn(*cargs, s_), name)

@@ -653,20 +653,28 @@ struct PackArgs {
   int cs[MAX_PACK], cb[MAX_PACK], kk[MAX_PACK];
   int n;
 };
+// walks each destination in its own order (coalesced stores; the 4-byte source gathers hit L2)
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   const int l = blockIdx.y;
   if (l >= a.n) return;
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
-  const long total = (long)cs * cbn * kk;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    // i enumerates the source W[cs][cb][tap]
-    const int tap = (int)(i % kk);
-    const long r = i / kk;
-    const int c_b = (int)(r % cbn), c_s = (int)(r / cbn);
-    const float v = a.src[l][i];
-    if (a.dg[l]) a.dg[l][((size_t)tap * cbn + c_b) * cs + c_s] = v;
-    if (a.ds[l]) a.ds[l][((size_t)tap * cs + c_s) * cbn + c_b] = v;
-  }
+  const int total = cs * cbn * kk;
+  const float* __restrict__ src = a.src[l];
+  const FDiv f_cs = FDiv::make(cs), f_cb = FDiv::make(cbn);
+  // gather copy [tap][cb][cs]
+  if (a.dg[l])
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+      const int q = f_cs.div(j), c_s = j - q * cs;  // q = tap*cbn + c_b
+      const int tap = f_cb.div(q), c_b = q - tap * cbn;
+      a.dg[l][j] = src[(c_s * cbn + c_b) * kk + tap];
+    }
+  // scatter copy [tap][cs][cb]
+  if (a.ds[l])
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+      const int q = f_cb.div(j), c_b = j - q * cbn;  // q = tap*cs + c_s
+      const int tap = f_cs.div(q), c_s = q - tap * cs;
+      a.ds[l][j] = src[(c_s * cbn + c_b) * kk + tap];
+    }
 }
 
 // ------------------------------------------------------------------ split-K reduction of WGRAD
@@ -1067,6 +1075,7 @@ extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_
     a.cb[i] = p.cb;
     a.kk[i] = p.kh * p.kw;
     const long tot = (long)p.cs * p.cb * p.kh * p.kw;
+    CV_REQUIRE(tot < (1L << 31), "pack_conv_weights: item %d too large", i);
     mx = tot > mx ? tot : mx;
   }
   a.n = n;

@@ -261,6 +261,7 @@ class ClearStep:
         dec = Program()
         ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False)
         ws.bn_grads_program(dec, pg, "dec")
+
         # latent terms -> d(heads)
         lat = Program()
         lat.add("cv_latent_combine", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),

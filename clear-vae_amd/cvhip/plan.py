@@ -352,15 +352,33 @@ def ep_bwd(bnv: BNView, ey: torch.Tensor, relu: bool, stat_div: int = 1) -> cv_e
 # ----------------------------------------------------------------------------- programs
 
 
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    key = torch.device(device).index
+    st = _SIDE_STREAMS.get(key)
+    if st is None:
+        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return st
+
+
 class Program:
-    """A fixed list of C-ABI calls (the stream is supplied at run time)."""
+    """A fixed list of C-ABI calls (the stream is supplied at run time).
+
+    Calls added with ``add_side`` run on a second stream: each forks from the main stream after the
+    main-stream calls issued before it (an event), consecutive side calls stay ordered among
+    themselves, and the main stream joins the side stream at the end of the program.  The backward
+    programs put the weight-gradient GEMMs there, so they overlap the next layer's data-gradient
+    GEMM instead of queueing behind it (both only read what the fork point has completed)."""
 
     def __init__(self):
-        self.calls = []
+        self.calls = []  # (name, fn, args, lane)
         self.keep = []  # keep ctypes structs alive
+        self._events = None
+        self.join_at_end = True
 
-    def add(self, name: str, *args):
-        fn = getattr(_lib.lib(), name)
+    def _conv(self, args):
         conv = []
         for a in args:
             if isinstance(a, ctypes.Structure):
@@ -370,18 +388,47 @@ class Program:
                 conv.append(a.data_ptr())
             else:
                 conv.append(a)
-        self.calls.append((name, fn, conv))
+        return conv
+
+    def add(self, name: str, *args):
+        self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 0))
+
+    def add_side(self, name: str, *args):
+        self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1))
 
     def extend(self, other: "Program"):
         self.calls += other.calls
         self.keep += other.keep
 
-    def run(self, stream: int | None = None):
+    def run(self, stream: int | None = None, join: bool | None = None):
+        """join=False leaves the side stream running past the end of the program (a later program's
+        run joins it: the side stream is one ordered queue); graph capture needs a join before its end."""
         s = _lib.stream_handle() if stream is None else stream
-        for name, fn, args in self.calls:
-            rc = fn(*args, s)
+        if not any(c[3] for c in self.calls):
+            for name, fn, args, _ in self.calls:
+                rc = fn(*args, s)
+                if rc != 0:
+                    _lib.check(rc, name)
+            return
+        main = torch.cuda.current_stream()
+        side = _side_stream(main.device)
+        if self._events is None:  # created on the first (eager) run, reused by graph capture
+            nf = sum(1 for i, c in enumerate(self.calls) if c[3] and (i == 0 or not self.calls[i - 1][3]))
+            self._events = [torch.cuda.Event() for _ in range(nf + 1)]
+        ev = 0
+        prev_lane = 0
+        for name, fn, args, lane in self.calls:
+            if lane and not prev_lane:  # fork: the side stream waits for the main-stream work so far
+                self._events[ev].record(main)
+                side.wait_event(self._events[ev])
+                ev += 1
+            rc = fn(*args, side.cuda_stream if lane else s)
             if rc != 0:
                 _lib.check(rc, name)
+            prev_lane = lane
+        if self.join_at_end if join is None else join:
+            self._events[ev].record(side)
+            main.wait_event(self._events[ev])
 
 
 def struct_array(ctype, items):
@@ -552,8 +599,8 @@ class Workspace:
             else:
                 P.add("cv_conv_backward_data", g, gout, c.wbwd, self.gah, ep_none())
                 xin = operand(self.ah)
-            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
-                  self.wg_bytes)
+            P.add_side("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
+                       self.wg_bytes)
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
         P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
@@ -569,8 +616,8 @@ class Workspace:
         C, Hh, Wh = sp.feat
         lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
         a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
-        P.add("cv_linear_backward_weight", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
-              param_grad(sp.heads[0].bias), 0, self.wg_work, self.wg_bytes)
+        P.add_side("cv_linear_backward_weight", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
+                   param_grad(sp.heads[0].bias), 0, self.wg_work, self.wg_bytes)
         ep = ep_bwd(self.bn_enc[-1], self.y_enc[-1], True, stat_div=Hh * Wh)
         P.add("cv_linear_backward_data", lin, operand(dheads), sp.heads[0].weight, self.g_enc[-1], 0, ep)
         for li in range(len(sp.enc) - 1, -1, -1):
@@ -585,8 +632,8 @@ class Workspace:
                 if dx is not None:
                     P.add("cv_conv_backward_data", g, gout, c.wbwd, dx, ep_none())
                 xin = operand(x, nchw=1)
-            P.add("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
-                  self.wg_bytes)
+            P.add_side("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
+                       self.wg_bytes)
 
     def bn_grads_program(self, P: Program, param_grad, which: str = "all"):
         views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
