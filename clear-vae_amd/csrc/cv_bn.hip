@@ -277,18 +277,57 @@ __device__ __forceinline__ int dl_feature(int col, int pix, int ch) {
 
 constexpr int DL_RPT = DL_R / 4;  // rows per thread (4 row groups per block)
 
+// The block's 64 storage columns map to features dl_feature(col) that are pix apart, so a per-thread
+// replica fold would issue 2-4 uncoalesced fp64 loads per replica in every thread.  Instead the 4 row
+// groups each fold every 4th replica of the 64 features and the partials meet in LDS (fixed order).
+__device__ __forceinline__ void dl_fold(const cv_bn& b, bool bwd, int f, bool live, double (*part)[4][DL_F],
+                                        BnFwdC* kf, BnBwdC* kb) {
+  const int t = threadIdx.x, cl = t % DL_F, rg = t / DL_F;
+  const int F = b.C, R = CV_STAT_REPL(F);
+  double s = 0.0, q = 0.0, gs = 0.0, gq = 0.0;
+  if (live && b.train)
+    for (int r = rg; r < R; r += 4) {
+      s += b.stat[(size_t)r * 2 * F + f];
+      q += b.stat[(size_t)r * 2 * F + F + f];
+      if (bwd) {
+        gs += b.gstat[(size_t)r * 2 * F + f];
+        gq += b.gstat[(size_t)r * 2 * F + F + f];
+      }
+    }
+  part[0][rg][cl] = s;
+  part[1][rg][cl] = q;
+  part[2][rg][cl] = gs;
+  part[3][rg][cl] = gq;
+  __syncthreads();
+  if (t < DL_F) {
+    double S = 0.0, Q = 0.0, GS = 0.0, GQ = 0.0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      S += part[0][g][t];
+      Q += part[1][g][t];
+      GS += part[2][g][t];
+      GQ += part[3][g][t];
+    }
+    if (live) {
+      if (bwd) kb[t] = bn_bwd_const_s(b, f, S, Q, GS, GQ);
+      else kf[t] = bn_fwd_const_s(b, f, S, Q);
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int pix, int ch, float* da,
                                                              const float* __restrict__ h, const cv_bn b,
                                                              double* gstat) {
   __shared__ float r1[4][DL_F], r2[4][DL_F];
   __shared__ int fidx[DL_F];
+  __shared__ double part[4][4][DL_F];
+  __shared__ BnFwdC kf[DL_F];
   const int t = threadIdx.x;
   const int c0 = blockIdx.x * DL_F, rbase = blockIdx.y * DL_R;
   const int cl = t % DL_F, rg = t / DL_F;
   const int col = c0 + cl;
   const int f = col < F ? dl_feature(col, pix, ch) : 0;
-  BnFwdC k;
-  if (col < F) k = bn_fwd_const(b, f);
   float hv[DL_RPT], dv[DL_RPT];
 #pragma unroll
   for (int i = 0; i < DL_RPT; ++i) {  // issue every load of the column slice first
@@ -300,6 +339,9 @@ __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int p
       dv[i] = da[(size_t)r * F + col];
     }
   }
+  dl_fold(b, false, f, col < F, part, kf, nullptr);
+  BnFwdC k;
+  if (col < F) k = kf[cl];
   float s1 = 0.f, s2 = 0.f;
   if (col < F) {
 #pragma unroll
@@ -324,7 +366,6 @@ __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int p
     atomic_add_f64(gstat + (size_t)repl * 2 * F + fidx[t], a);
     atomic_add_f64(gstat + (size_t)repl * 2 * F + F + fidx[t], q);
   }
-  __shared__ double scratch[4 * 256];
 }
 
 template <int KPT>
@@ -334,13 +375,13 @@ __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int 
                                                               const float* __restrict__ z, float* gw) {
   __shared__ float sd[DL_R][DL_F + 1];
   __shared__ float sz[DL_R][4 * KPT + 1];
+  __shared__ double part[4][4][DL_F];
+  __shared__ BnBwdC kbs[DL_F];
   const int t = threadIdx.x;
   const int c0 = blockIdx.x * DL_F, r0 = blockIdx.y * DL_R;
   const int cl = t % DL_F, rg = t / DL_F;
   const int col = c0 + cl;
   const int f = col < F ? dl_feature(col, pix, ch) : 0;
-  BnBwdC kb;
-  if (col < F) kb = bn_bwd_const(b, f);
   float dv[DL_RPT], hv[DL_RPT];
 #pragma unroll
   for (int i = 0; i < DL_RPT; ++i) {
@@ -360,6 +401,9 @@ __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int 
     const int rr = e / (4 * KPT), kk = e % (4 * KPT);
     zv[j] = (e < DL_R * 4 * KPT && r0 + rr < n && kk < K) ? z[(size_t)(r0 + rr) * K + kk] : 0.f;
   }
+  dl_fold(b, true, f, col < F, part, nullptr, kbs);
+  BnBwdC kb;
+  if (col < F) kb = kbs[cl];
 #pragma unroll
   for (int i = 0; i < DL_RPT; ++i) {
     const int r = r0 + rg + 4 * i;

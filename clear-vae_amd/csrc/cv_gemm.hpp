@@ -796,6 +796,15 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
       return 1;
     }
   }
+  if (g_fast_occ_query) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, NT, lds) != hipSuccess) {
+      (void)hipGetLastError();
+      nb = 0;
+    }
+    *g_fast_occ_query = nb;
+    return 0;
+  }
   hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
   CV_LAUNCH_CHECK("gemm");
   return 0;

@@ -775,6 +775,38 @@ static void finalize_divs(Args& a) {
 // 1: route every call to the generic kernel (kernel-variant comparisons in tests only)
 static int g_force_generic = 0;
 
+thread_local int* g_fast_occ_query = nullptr;
+
+// resident workgroups per CU of the specialised-core kernel a launch with this tile would pick
+// (0 when the generic kernel would serve it)
+static int fast_occupancy(const Args& a0, int BM_, int BN_) {
+  if (g_force_generic) return 0;
+  Args a = a0;
+  finalize_divs(a);
+  int occ = 0;
+  g_fast_occ_query = &occ;
+  const dim3 grid(1, 1, 1);
+  int r = -1;
+  switch (a.op) {
+    case OP_GATHER: r = gemm_fast_gather(a, BM_, BN_, grid, nullptr); break;
+    case OP_SCATTER: r = gemm_fast_scatter(a, BM_, BN_, grid, nullptr); break;
+    case OP_WGRAD: r = gemm_fast_wgrad(a, BM_, BN_, grid, nullptr); break;
+    default: r = gemm_fast_dense(a, BM_, BN_, grid, nullptr); break;
+  }
+  g_fast_occ_query = nullptr;
+  return r >= 0 ? occ : 0;
+}
+
+static int device_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
   finalize_divs(a);
   const int Ntot = a.N + ((a.op == OP_WGRAD && a.gbias) ? 1 : 0);
@@ -1031,9 +1063,23 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   a.N = g.kh * g.kw * g.cb;
   CV_REQUIRE(!gbias || (a.N % 4) == 0, "wgrad: bias column needs taps*channels % 4 == 0");
   a.K = g.n * g.hs * g.ws;
-  const WPlan w = wgrad_plan(a.M, a.N, a.K, split_k);
-  a.kchunk = w.kchunk;
+  WPlan w = wgrad_plan(a.M, a.N, a.K, split_k);
   const int Ntot = a.N + (gbias ? 1 : 0);
+  if (split_k <= 0 && w.split > 1) {
+    // one round of resident workgroups: a second, partial round costs a whole extra workgroup time
+    // (prologue + K loop + epilogue) while fewer, longer splits only lengthen the K loop
+    const long tiles = (long)cdiv(a.M, w.BM) * cdiv(Ntot, w.BN);
+    a.kchunk = w.kchunk;
+    a.gbias = gbias;
+    const int occ = fast_occupancy(a, w.BM, w.BN);
+    const long slots = (long)device_cus() * occ;
+    if (occ > 0 && tiles * w.split > slots && tiles <= slots) {
+      const long s2 = slots / tiles;
+      w.kchunk = (int)(((a.K + s2 - 1) / s2 + BK - 1) / BK) * BK;
+      w.split = (int)((a.K + w.kchunk - 1) / w.kchunk);
+    }
+  }
+  a.kchunk = w.kchunk;
   if (w.split > 1 && work) {
     const size_t need = (size_t)w.split * a.M * Ntot * sizeof(float);
     CV_REQUIRE(work_bytes >= need, "wgrad: workspace %zu bytes < %zu needed", work_bytes, need);

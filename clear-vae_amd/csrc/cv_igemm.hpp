@@ -103,5 +103,8 @@ int gemm_fast_gather(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
 int gemm_fast_scatter(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
 int gemm_fast_wgrad(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
 int gemm_fast_dense(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
+// occupancy query: while non-null, a gemm_fast_* call that would launch stores the chosen kernel's
+// resident workgroups per CU here instead (and launches nothing)
+extern thread_local int* g_fast_occ_query;
 
 }  // namespace cv
