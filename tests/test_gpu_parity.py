@@ -302,3 +302,38 @@ def test_trainer_fit_decreases_loss():
     assert tr.annealer.current_step == 9 * 4
     st = tr.optimizer.state[next(tr.model.parameters())]
     assert int(float(st["step"])) == 36
+
+
+@pytest.mark.parametrize("arch,n,zt,C", [("VAE", 64, 16, 1), ("VAE", 37, 16, 1), ("VAE64", 16, 64, 3)])
+def test_eval_mode_forward(arch, n, zt, C):
+    """the eval-mode forward of `evaluate()` (BatchNorm on the running statistics,
+    no grad) through the HIP kernels, vs the oracle's eval-mode forward on the same weights and noise;
+    the running statistics must not move."""
+    from oracle import cpu_ref as R
+    from cvhip import rng
+    from src.losses import vae_loss
+
+    sd = R.det_state(arch, zt, C)  # non-trivial running statistics
+    x, label, ec, es, perm = R.det_inputs(n, C, R.IMAGE[arch], zt, 10)
+    vae = _model(arch, zt, C, sd)
+    vae.eval()
+    before = {k: v.clone() for k, v in vae.state_dict().items() if "running" in k or "num_batches" in k}
+    X = torch.tensor(x, dtype=torch.float32, device="cuda")
+    rng.clear_injections()
+    rng.inject_noise([torch.tensor(ec, dtype=torch.float32), torch.tensor(es, dtype=torch.float32)])
+    with torch.no_grad():
+        xhat, lp, z = vae(X, explicit=True)
+        rec, kl_c, kl_s = vae_loss(xhat, X, **lp)
+    P = R.to_torch(sd, requires_grad=False)
+    oxhat, olp, oz = R.vae_forward(P, torch.tensor(x, dtype=torch.float64), torch.tensor(ec), torch.tensor(es), arch,
+                                   train=False)
+    orec, okc, oks = R.vae_loss(oxhat, torch.tensor(x, dtype=torch.float64), **olp)
+    for k in ("mu_c", "logvar_c", "mu_s", "logvar_s"):
+        assert _rel(lp[k], olp[k]) < LOSS_TOL, k
+    assert _rel(z, oz) < LOSS_TOL
+    assert _rel(xhat, oxhat) < LOSS_TOL
+    for a, b, nm in ((rec, orec, "rec"), (kl_c, okc, "kl_c"), (kl_s, oks, "kl_s")):
+        assert abs(float(a) - float(b)) <= LOSS_TOL * max(abs(float(b)), 1e-3), (nm, float(a), float(b))
+    for k, v in vae.state_dict().items():
+        if k in before:
+            assert torch.equal(v, before[k]), k
