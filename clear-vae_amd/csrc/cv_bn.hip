@@ -580,17 +580,22 @@ extern "C" int cv_output_backward(const cv_bn* bn, const float* y, const float* 
 extern "C" int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, const cv_bn* bn,
                                             double* gstat_out, const float* zin, float* gweight, cv_stream_t stream) {
   clear_error();
-  CV_REQUIRE(g && da && h && bn && gstat_out && zin && gweight, "declinear_backward_weight: null args");
+  CV_REQUIRE(g && da && h && bn && (gstat_out || gweight), "declinear_backward_weight: null args");
+  CV_REQUIRE(!gweight || zin, "declinear_backward_weight: the weight gradient needs z");
   CV_REQUIRE(g->in_features <= 128, "declinear_backward_weight: latent width %d > 128", g->in_features);
   CV_REQUIRE(bn->C == g->out_features && bn->train, "declinear_backward_weight: BN1d must be train-mode, C=out");
   const int pix = g->out_pix > 0 ? g->out_pix : 1;
   const int F = g->out_features, K = g->in_features;
   dim3 grid(cdiv(F, DL_F), cdiv(g->n, DL_R));
-  hipLaunchKernelGGL(declinear_mask_kernel, grid, dim3(256), 0, S(stream), g->n, F, pix, g->out_ch, da, h, *bn,
-                     gstat_out);
-  CV_LAUNCH_CHECK("declinear_mask");
+  if (gstat_out) {  // mask + BN1d backward sums
+    hipLaunchKernelGGL(declinear_mask_kernel, grid, dim3(256), 0, S(stream), g->n, F, pix, g->out_ch, da, h, *bn,
+                       gstat_out);
+    CV_LAUNCH_CHECK("declinear_mask");
+  }
+  if (!gweight) return 0;
   cv_bn b2 = *bn;
-  b2.gstat = gstat_out;
+  if (gstat_out) b2.gstat = gstat_out;  // (else: da already masked, bn->gstat complete)
+  CV_REQUIRE(b2.gstat != nullptr, "declinear_backward_weight: BN1d backward sums missing");
   if (K <= 16)
     hipLaunchKernelGGL(declinear_wgrad_kernel<4>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
                        b2, zin, gweight);

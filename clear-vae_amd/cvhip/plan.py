@@ -554,11 +554,13 @@ class Workspace:
         P.add("cv_reparam_forward", self.heads, self.n, self.spec.d, eps.data_ptr() if eps is not None else None,
               ctypes.c_uint64(seed), offset.data_ptr() if offset is not None else None, self.z, None)
 
-    def running_program(self, P: Program, which: str = "all"):
+    def running_program(self, P: Program, which: str = "all", side: bool = False):
+        """side=True: on the side stream (only where nothing re-zeroes the statistics before a join)."""
         views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
         bns = struct_array(cv_bn, [b.cv(True) for b in views])
         nbt = ptr_array([b.mod.num_batches_tracked.data_ptr() for b in views])
-        P.add("cv_bn_update_running", bns, len(views), ctypes.c_float(float(views[0].mod.momentum)), nbt)
+        (P.add_side if side else P.add)("cv_bn_update_running", bns, len(views),
+                                        ctypes.c_float(float(views[0].mod.momentum)), nbt)
 
     def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None):
         sp, n = self.spec, self.n
@@ -635,9 +637,9 @@ class Workspace:
             P.add_side("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
                        self.wg_bytes)
 
-    def bn_grads_program(self, P: Program, param_grad, which: str = "all"):
+    def bn_grads_program(self, P: Program, param_grad, which: str = "all", side: bool = False):
         views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
         bns = struct_array(cv_bn, [b.cv(True) for b in views])
         dg = ptr_array([param_grad(b.mod.weight) for b in views])
         db = ptr_array([param_grad(b.mod.bias) for b in views])
-        P.add("cv_bn_param_grads", bns, len(views), dg, db)
+        (P.add_side if side else P.add)("cv_bn_param_grads", bns, len(views), dg, db)

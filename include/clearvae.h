@@ -162,7 +162,9 @@ int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const 
  * output in the Unflatten/NHWC order (g->out_pix, g->out_ch); h: the Linear output (BN1d input),
  * same order.  Two launches: (1) mask da in place (da <- dz) and accumulate the BN1d backward sums
  * into gstat_out (fp64, replicas; caller zeroes); (2) accumulate the Linear weight gradient
- * dW[f][k] += sum_n BNbwd(dz)[n][f] * zin[n][k] (caller zeroes). */
+ * dW[f][k] += sum_n BNbwd(dz)[n][f] * zin[n][k] (caller zeroes).  gweight == NULL runs only (1);
+ * gstat_out == NULL runs only (2) on an already masked da with bn->gstat holding the sums (so the
+ * weight gradient can run off the critical path, on another stream, after (1)). */
 int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, const cv_bn* bn,
                                  double* gstat_out, const float* zin, float* gweight,
                                  cv_stream_t stream);
