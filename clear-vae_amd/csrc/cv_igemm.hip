@@ -833,12 +833,21 @@ static int launch(Args& a, int BM_, int BN_, int gz, hipStream_t st) {
 }
 
 // Row-oriented tile: prefer 64-wide N tiles, shrink N (keeping BM=64) until there are >= 512
-// workgroups; BM=128 only for very tall problems.  (Measured against BM=128-first and >=256/384/768/
-// 1024-workgroup variants on both bench configs: this one is best or within noise.)
+// workgroups (measured against 256/384/768/1024-workgroup targets on both bench configs: best or
+// within noise).  BM=128 lost everywhere once the BM=64 narrow variants hold 3 workgroups per CU
+// (VAE64 conv1 bwd-data 170 -> 112 us, convT4 fwd 92 -> 79 us).
 static void pick_tile(long M, int N, int& BM_, int& BN_) {
+  // A/B overrides: CV_BM128_MIN (rows from which BM=128 is used), CV_MIN_BLOCKS (N-shrink target)
+  static long bm128_min = -1, min_blocks = -1;
+  if (bm128_min < 0) {
+    const char* e = getenv("CV_BM128_MIN");
+    bm128_min = e ? atol(e) : (1L << 40);
+    const char* f = getenv("CV_MIN_BLOCKS");
+    min_blocks = f ? atol(f) : 512;
+  }
   BN_ = (N <= 16) ? 16 : (N <= 32) ? 32 : 64;
-  BM_ = (M >= 128L * 1024) ? 128 : 64;
-  while (BN_ > 16 && (long)cdiv(M, BM_) * cdiv(N, BN_) < 512) BN_ >>= 1;
+  BM_ = (M >= bm128_min) ? 128 : 64;
+  while (BN_ > 16 && (long)cdiv(M, BM_) * cdiv(N, BN_) < min_blocks) BN_ >>= 1;
 }
 
 // number of K splits: aim for ~1024 workgroups but keep >= 4 K tiles per split
