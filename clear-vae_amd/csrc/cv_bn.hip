@@ -453,9 +453,49 @@ __global__ __launch_bounds__(256) void zero_many_kernel(const ZeroArgs z) {
   }
 }
 
+struct CopyArgs {
+  uint32_t* dst[8];
+  const uint32_t* src[8];
+  long start[9];  // prefix sums of the 4-byte word counts
+  int count;
+};
+
+__global__ __launch_bounds__(256) void copy_many_kernel(const CopyArgs c) {
+  const long total = c.start[c.count];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int b = 0;
+#pragma unroll
+    for (int q = 1; q < 8; ++q)
+      if (q < c.count && i >= c.start[q]) b = q;
+    c.dst[b][i - c.start[b]] = c.src[b][i - c.start[b]];
+  }
+}
+
 }  // namespace cv
 
 using namespace cv;
+
+extern "C" int cv_copy_many(void* const* dst, const void* const* src, const size_t* bytes, int count,
+                            cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(dst && src && bytes && count > 0 && count <= 8, "copy_many: 1..8 buffers");
+  CopyArgs c;
+  memset(&c, 0, sizeof(c));
+  c.count = count;
+  for (int i = 0; i < count; ++i) {
+    CV_REQUIRE(dst[i] && src[i] && bytes[i] % 4 == 0 && ((uintptr_t)dst[i] | (uintptr_t)src[i]) % 4 == 0,
+               "copy_many: buffer %d not 4-byte granular", i);
+    c.dst[i] = (uint32_t*)dst[i];
+    c.src[i] = (const uint32_t*)src[i];
+    c.start[i + 1] = c.start[i] + (long)(bytes[i] / 4);
+  }
+  long g = (c.start[count] + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(copy_many_kernel, dim3((int)g), dim3(256), 0, S(stream), c);
+  CV_LAUNCH_CHECK("copy_many");
+  return 0;
+}
 
 extern "C" int cv_zero_many(void* const* ptrs, const size_t* bytes, int count, cv_stream_t stream) {
   clear_error();

@@ -156,8 +156,12 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
 #ifndef CV_FAST_MINW_SMALL
 #define CV_FAST_MINW_SMALL 3
 #endif
+#ifndef CV_FAST_MINW_64
+#define CV_FAST_MINW_64 1
+#endif
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int D>
-__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? CV_FAST_MINW_SMALL : 1) void gemm_kernel(const Args P) {
+__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? CV_FAST_MINW_SMALL : (BM == 64 ? CV_FAST_MINW_64 : 1))
+void gemm_kernel(const Args P) {
   using SH = Shape<OP, BM, BN>;
   constexpr int WN = SH::WN, WM = SH::WM, TM = SH::TM, TN = SH::TN, FM = SH::FM, FN = SH::FN;
   constexpr int RA = SH::RA, RB = SH::RB;

@@ -215,6 +215,7 @@ _SIGS = {
     "cv_bn_param_grads": (c_int, [_P(cv_bn), c_int, _P(c_void_p), _P(c_void_p), c_void_p]),
     "cv_zero": (c_int, [c_void_p, c_size_t, c_void_p]),
     "cv_zero_many": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "cv_copy_many": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "cv_last_error": (ctypes.c_char_p, []),
     "cv_version": (c_int, []),
     "cv_debug_force_generic_gemm": (c_int, [c_int]),

@@ -422,6 +422,19 @@ class ClearStep:
         G["graphs"] = graphs
 
     # ----------------------------------------------------------------------------- one step
+    def _load_batch(self, G, X, label):
+        """Copy the batch into the graph's static input buffers (one launch when no conversion is needed)."""
+        lab = label.reshape(-1)
+        if (X.dtype == torch.float32 and X.is_contiguous() and X.device == G["X"].device and lab.dtype == torch.int64
+                and lab.is_contiguous() and lab.device == G["lab"].device):
+            dst = ptr_array([G["X"].data_ptr(), G["lab"].data_ptr()])
+            src = ptr_array([X.data_ptr(), lab.data_ptr()])
+            nb = (ctypes.c_size_t * 2)(G["X"].numel() * 4, G["lab"].numel() * 8)
+            _lib.call("cv_copy_many", dst, src, nb, 2, _lib.stream_handle())
+        else:
+            G["X"].copy_(X, non_blocking=True)
+            G["lab"].copy_(lab, non_blocking=True)
+
     def step(self, X, label):
         n = X.shape[0]
         G = self.graphs.get(n)
@@ -432,8 +445,7 @@ class ClearStep:
         self.adam.refresh_hyper()
         if self.mode == "mim":
             self.est_adam.refresh_hyper()
-        G["X"].copy_(X, non_blocking=True)
-        G["lab"].copy_(label.reshape(-1), non_blocking=True)
+        self._load_batch(G, X, label)
         inject = self._take_injections(G)
         use_graph = G["count"] >= 1 and not inject and self.graphs_enabled
         if use_graph and "graphs" not in G:

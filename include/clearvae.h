@@ -312,6 +312,8 @@ int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dgamma, float*
 int cv_zero(void* ptr, size_t bytes, cv_stream_t stream);
 /* zero up to 8 buffers (4-byte granular: sizes multiples of 4, 4-byte aligned) in one launch */
 int cv_zero_many(void* const* ptrs, const size_t* bytes, int count, cv_stream_t stream);
+/* device-to-device copy of up to 8 buffers (4-byte granular) in one launch (the step's input batch) */
+int cv_copy_many(void* const* dst, const void* const* src, const size_t* bytes, int count, cv_stream_t stream);
 const char* cv_last_error(void);
 int cv_version(void);
 /* test hook: 1 routes every conv/linear GEMM to the generic implicit-GEMM kernel instead of the
