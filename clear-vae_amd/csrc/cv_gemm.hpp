@@ -783,6 +783,9 @@ void gemm_kernel(const Args P) {
 #endif
 }
 
+#ifndef CV_FAST_DEPTH_BNBWD
+#define CV_FAST_DEPTH_BNBWD 2
+#endif
 #ifndef CV_FAST_DEPTH
 #define CV_FAST_DEPTH 3
 #endif
@@ -796,7 +799,10 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
   const size_t lds = fast_lds_floats(BM, BN, soa_arrays<XA>() * nfa, soa_arrays<XFB>() * nfb,
                                      EPI == CV_STAT_BWD ? 4 * a.ce_n : 0) * sizeof(float);
   CV_REQUIRE(lds <= 160 * 1024, "gemm: LDS request %zu bytes exceeds 160 KiB", lds);
-  auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, CV_FAST_DEPTH>;
+  // the BN-backward A operand doubles the ring's registers: a 2-deep ring keeps the narrow tiles at
+  // 3 resident workgroups per CU without spilling
+  constexpr int DEPTH = (XA == CV_XF_BNBWD && BM == 64 && BN <= 32) ? CV_FAST_DEPTH_BNBWD : CV_FAST_DEPTH;
+  auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, DEPTH>;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) {
