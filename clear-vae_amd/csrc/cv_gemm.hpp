@@ -162,6 +162,7 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int D>
 __global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? CV_FAST_MINW_SMALL : (BM == 64 ? CV_FAST_MINW_64 : 1))
 void gemm_kernel(const Args P) {
+  static_assert(D >= 2, "the register ring needs at least two stages (D=1 is not a valid schedule)");
   using SH = Shape<OP, BM, BN>;
   constexpr int WN = SH::WN, WM = SH::WM, TM = SH::TM, TN = SH::TN, FM = SH::FM, FN = SH::FN;
   constexpr int RA = SH::RA, RB = SH::RB;
@@ -787,7 +788,7 @@ void gemm_kernel(const Args P) {
 #define CV_FAST_DEPTH_BNBWD 2
 #endif
 #ifndef CV_FAST_DEPTH
-#define CV_FAST_DEPTH 3
+#define CV_FAST_DEPTH 2
 #endif
 
 template <int OP, int BM, int BN, int XA, int XB, int EPI>
