@@ -787,6 +787,9 @@ void gemm_kernel(const Args P) {
 #ifndef CV_FAST_DEPTH_BNBWD
 #define CV_FAST_DEPTH_BNBWD 2
 #endif
+#ifndef CV_FAST_DEPTH_WGRAD
+#define CV_FAST_DEPTH_WGRAD 3
+#endif
 #ifndef CV_FAST_DEPTH
 #define CV_FAST_DEPTH 2
 #endif
@@ -802,7 +805,10 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
   CV_REQUIRE(lds <= 160 * 1024, "gemm: LDS request %zu bytes exceeds 160 KiB", lds);
   // the BN-backward A operand doubles the ring's registers: a 2-deep ring keeps the narrow tiles at
   // 3 resident workgroups per CU without spilling
-  constexpr int DEPTH = (XA == CV_XF_BNBWD && BM == 64 && BN <= 32) ? CV_FAST_DEPTH_BNBWD : CV_FAST_DEPTH;
+  // the long-K weight-gradient tiles keep a 3-deep ring (one workgroup per CU there anyway)
+  constexpr int DEPTH = (XA == CV_XF_BNBWD && BM == 64 && BN <= 32) ? CV_FAST_DEPTH_BNBWD
+                        : (OP == OP_WGRAD && BM == 128)            ? CV_FAST_DEPTH_WGRAD
+                                                                   : CV_FAST_DEPTH;
   auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, DEPTH>;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
