@@ -653,28 +653,62 @@ struct PackArgs {
   int cs[MAX_PACK], cb[MAX_PACK], kk[MAX_PACK];
   int n;
 };
-// walks each destination in its own order (coalesced stores; the 4-byte source gathers hit L2)
-__global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
+// small layers: one destination element per thread, each destination walked in its own order
+__global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
   const int l = blockIdx.y;
   if (l >= a.n) return;
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
   const int total = cs * cbn * kk;
   const float* __restrict__ src = a.src[l];
   const FDiv f_cs = FDiv::make(cs), f_cb = FDiv::make(cbn);
-  // gather copy [tap][cb][cs]
-  if (a.dg[l])
-    for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
-      const int q = f_cs.div(j), c_s = j - q * cs;  // q = tap*cbn + c_b
-      const int tap = f_cb.div(q), c_b = q - tap * cbn;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+    if (a.dg[l]) {  // [tap][cb][cs]
+      const int q = f_cs.div(j), c_s = j - q * cs, tap = f_cb.div(q), c_b = q - tap * cbn;
       a.dg[l][j] = src[(c_s * cbn + c_b) * kk + tap];
     }
-  // scatter copy [tap][cs][cb]
-  if (a.ds[l])
-    for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
-      const int q = f_cb.div(j), c_b = j - q * cbn;  // q = tap*cs + c_s
-      const int tap = f_cs.div(q), c_s = q - tap * cs;
+    if (a.ds[l]) {  // [tap][cs][cb]
+      const int q = f_cb.div(j), c_b = j - q * cbn, tap = f_cs.div(q), c_s = q - tap * cs;
       a.ds[l][j] = src[(c_s * cbn + c_b) * kk + tap];
     }
+  }
+}
+
+// LDS-tiled transpose: a workgroup stages a 16 (cs) x 32 (cb) x taps block of W[cs][cb][tap] with
+// coalesced loads (each cs row of the block is 32*taps contiguous floats), then writes both copies
+// from LDS in their own orders: Wg[tap][cb][cs] in runs of 16 cs, Ws[tap][cs][cb] in runs of 32 cb.
+constexpr int PK_CS = 16, PK_CB = 32, PK_MAXK = 16;
+__global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
+  __shared__ float tile[PK_CS * PK_CB * (PK_MAXK + 1)];
+  const int l = blockIdx.y;
+  if (l >= a.n) return;
+  const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
+  const int tcb = (cbn + PK_CB - 1) / PK_CB;
+  const int ntile = ((cs + PK_CS - 1) / PK_CS) * tcb;
+  const float* __restrict__ src = a.src[l];
+  const int pitch = kk + 1;  // odd: the column walks below hit distinct banks
+  for (int tile_id = blockIdx.x; tile_id < ntile; tile_id += gridDim.x) {
+    const int cs0 = (tile_id / tcb) * PK_CS, cb0 = (tile_id % tcb) * PK_CB;
+    const int ncs = min(PK_CS, cs - cs0), ncb = min(PK_CB, cbn - cb0);
+    const int run = ncb * kk;  // contiguous floats per cs row of the block
+    const FDiv f_run = FDiv::make(run), f_kk = FDiv::make(kk), f_cs = FDiv::make(ncs), f_cb = FDiv::make(ncb);
+    for (int e = threadIdx.x; e < ncs * run; e += 256) {
+      const int i = f_run.div(e), r = e - i * run;  // r = (cb - cb0)*kk + tap
+      const int j = f_kk.div(r), tap = r - j * kk;
+      tile[(i * PK_CB + j) * pitch + tap] = src[((size_t)(cs0 + i) * cbn + cb0) * kk + r];
+    }
+    __syncthreads();
+    if (a.dg[l])  // [tap][cb][cs]: runs of ncs
+      for (int e = threadIdx.x; e < kk * ncb * ncs; e += 256) {
+        const int q = f_cs.div(e), i = e - q * ncs, tap = f_cb.div(q), j = q - tap * ncb;
+        a.dg[l][((size_t)tap * cbn + cb0 + j) * cs + cs0 + i] = tile[(i * PK_CB + j) * pitch + tap];
+      }
+    if (a.ds[l])  // [tap][cs][cb]: runs of ncb
+      for (int e = threadIdx.x; e < kk * ncs * ncb; e += 256) {
+        const int q = f_cb.div(e), j = e - q * ncb, tap = f_cs.div(q), i = q - tap * ncs;
+        a.ds[l][((size_t)tap * cs + cs0 + i) * cbn + cb0 + j] = tile[(i * PK_CB + j) * pitch + tap];
+      }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------ split-K reduction of WGRAD
@@ -1134,9 +1168,17 @@ extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_
     mx = tot > mx ? tot : mx;
   }
   a.n = n;
-  long gx = (mx + 255) / 256;
+  bool tiled = mx >= 256 * 1024;  // big layers: the LDS-tiled transpose; small ones: more parallelism
+  long gx = 1;
+  for (int i = 0; i < n; ++i) {
+    if (a.kk[i] > PK_MAXK) tiled = false;
+    const long t = (long)cdiv(a.cs[i], PK_CS) * cdiv(a.cb[i], PK_CB);
+    gx = t > gx ? t : gx;
+  }
+  if (!tiled) gx = (mx + 255) / 256;
   if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(pack_kernel, dim3(gx, n), dim3(256), 0, S(stream), a);
+  if (tiled) hipLaunchKernelGGL(pack_kernel, dim3((int)gx, n), dim3(256), 0, S(stream), a);
+  else hipLaunchKernelGGL(pack_small_kernel, dim3((int)gx, n), dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("pack_conv_weights");
   return 0;
 }
