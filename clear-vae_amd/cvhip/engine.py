@@ -152,8 +152,9 @@ class ClearStep:
         self.sim = SIM[trainer.sim_fn]
         self.anneal = torch.tensor([trainer.annealer.current_step], dtype=torch.int64, device=self.device)
         self.anneal_expected = trainer.annealer.current_step
-        self.seed, _ = rng.offset_tensor(self.device)
-        self.offset = torch.zeros(2, dtype=torch.int64, device=self.device)
+        # the shared (device, seed) Philox counter: engine rebuilds and the module path (evaluate, fallback
+        # steps) all advance one stream instead of replaying the same noise from 0
+        self.seed, self.offset = rng.offset_tensor(self.device)
         self.world = _dist_world()
         self.gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
         self.graphs = {}  # n -> dict

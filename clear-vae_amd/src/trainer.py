@@ -401,22 +401,33 @@ class LAMCNNTrainer(SimpleCNNTrainer):
         super().__init__(model, optimizer, criterion, verbose_period, device, transform)
         self.hyperparameter = hyperparameter
 
+    def ss_pairing(self, x, y):
+        """Stratified shuffle: every sample is paired with a random sample of the same label
+        (trainer.py:249-257)."""
+        new_x = x.clone()
+        for c in torch.unique(y):
+            idx = (y == c).nonzero(as_tuple=True)[0]
+            perm = torch.randperm(idx.shape[0])
+            new_x[idx] = x[idx[perm.to(idx.device)]]
+        return new_x
+
     def _train(self, dataloader: DataLoader, verbose: bool, epoch_id: int):
-        self.model.train()
+        """(X, y) batches, as the reference's callers pass them (trainer.py:259-288)."""
+        cnn = self.model
+        cnn.train()
         lam_coef = self.hyperparameter["lam_coef"]
         with tqdm(dataloader, unit="batch", disable=not verbose) as bar:
             bar.set_description(f"epoch {epoch_id}")
             for batch in bar:
-                X, X_tilde, y = batch[0], batch[1], batch[2].reshape(-1).long()
-                X, X_tilde, y = X.to(self.device), X_tilde.to(self.device), y.to(self.device)
+                X, y = _batch(batch, self.device, self.transform)
+                X_tilde = self.ss_pairing(X, y)
                 self.optimizer.zero_grad()
-                feat, feat_t = self.model.net(X), self.model.net(X_tilde)
-                logits = self.model.cls_head(feat)
-                loss = self.criterion(logits, y) + lam_coef * lam_loss(feat, feat_t, y, self.model.cls_head.weight)
+                loss_ce = self.criterion(cnn(X), y)
+                loss_lam = lam_loss(cnn.net(X), cnn.net(X_tilde), y, cnn.cls_head.weight)
+                loss = loss_ce + lam_coef * loss_lam
                 loss.backward()
                 self.optimizer.step()
-                if verbose:
-                    bar.set_postfix(loss=float(loss))
+                bar.set_postfix(ce_loss=float(loss_ce), lam_loss=float(loss_lam))
 
 
 class HierarchicalVAETrainer(VAETrainer):

@@ -1,0 +1,184 @@
+"""The fused engine's data-parallel step (cvhip/engine.py `_segments` / `make_learn_dp`), run as two
+processes on the one GPU over gloo (tests/dp_gpu_worker.py), against the DDP semantics of SURVEY §8(e):
+
+  * both ranks start from rank 0's parameters (rank 1 is built from different weights);
+  * each rank runs the step on its contiguous half of the global batch (local-batch BN / contrastive /
+    MI terms): its losses match the oracle on that shard;
+  * the gradient both ranks apply is the mean of the per-shard oracle gradients;
+  * the parameters after Adam are identical (bitwise) across ranks, equal to torch Adam applied to that
+    mean gradient, and stay identical through graph-captured replays;
+  * CLEAR-MIM: the estimator's 5 updates use the mean of the per-shard learning-loss gradients, and the
+    estimator parameters are identical across ranks.
+
+Tolerances are those of tests/test_gpu_parity.py (losses 1e-4 relative, gradient checks of
+`_check_grads`, Adam-step parameter checks)."""
+
+import multiprocessing as mp
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import dp_gpu_worker
+from test_gpu_parity import LOSS_TOL, _bias_before_bn, _check_grads
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(mode, n_global, kind="CLUBSample", world=2, timeout=100):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=dp_gpu_worker.run, args=(r, world, port, q, mode, n_global, kind))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, out, err = q.get(timeout=timeout)
+            assert err is None, err
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+def _adam_ref(sd, grads, lr=5e-4):
+    from oracle import cpu_ref as R
+
+    P0 = R.to_torch(sd, requires_grad=False)
+    names = list(grads)
+    ps = [P0[k].clone().requires_grad_(True) for k in names]
+    for p_, k in zip(ps, names):
+        p_.grad = torch.zeros_like(grads[k]) if _bias_before_bn(k, "VAE") else grads[k].clone()
+    torch.optim.Adam(ps, lr=lr).step()
+    return {k: p_.detach() for k, p_ in zip(names, ps)}
+
+
+def _rel(a, b):
+    a, b = torch.as_tensor(a).double().reshape(-1), torch.as_tensor(b).double().reshape(-1)
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _common_checks(res, sd, world=2):
+    # construction: every rank holds rank 0's weights
+    for k, v in res[0]["p0"].items():
+        assert np.array_equal(v, res[1]["p0"][k]), k
+        assert np.allclose(v, np.asarray(sd[k], dtype=np.float32), rtol=0, atol=0), k
+    # identical parameters after the DP Adam step and after two graph-replayed steps
+    for k in res[0]["p1"]:
+        assert np.array_equal(res[0]["p1"][k], res[1]["p1"][k]), k
+        assert np.array_equal(res[0]["grad"][k], res[1]["grad"][k]), k
+    assert np.array_equal(res[0]["p3"], res[1]["p3"])
+    assert res[0]["graphs"] and res[1]["graphs"], "DP segments were not graph-captured"
+    assert res[0]["opt_step"] == res[1]["opt_step"] == 3
+
+
+@pytest.mark.parametrize("n_global", [64, 50])
+def test_dp_clear_step_world2(n_global):
+    from oracle import cpu_ref as R
+
+    res = _launch("clear", n_global)
+    sd = R.det_state("VAE", 16, 1)
+    _common_checks(res, sd)
+    hp = {"temperature": 0.1, "alpha": 100.0, "beta": 0.125, "ps": True}
+    x, label, ec, es, _ = R.det_inputs(n_global, 1, 28, 16, 4, seed=21)
+    shards = []
+    for r in (0, 1):
+        lo, hi = res[r]["bounds"]
+        o = R.clear_step(R.to_torch(sd), torch.tensor(x[lo:hi]), torch.tensor(label[lo:hi]), torch.tensor(ec[lo:hi]),
+                         torch.tensor(es[lo:hi]), "VAE", hp)
+        shards.append(o)
+        got = res[r]["losses"]
+        for i, k in enumerate(("rec", "kl_c", "kl_s", "c_loss", "s_loss")):
+            ref = float(o[k])
+            assert abs(float(got[i]) - ref) <= LOSS_TOL * max(abs(ref), 1e-3), (r, k, float(got[i]), ref)
+    mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
+    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, "VAE")
+    ref_p = _adam_ref(sd, mean_g)
+    prel = sorted((_rel(res[0]["p1"][k], ref_p[k]), k) for k in ref_p)
+    assert prel[len(prel) // 2][0] < 1e-5, prel[-3:]
+    assert prel[-1][0] < 5e-3, prel[-3:]
+
+
+@pytest.mark.parametrize("kind", ["CLUBSample", "L1OutUB"])
+def test_dp_mim_step_world2(kind):
+    from oracle import cpu_ref as R
+
+    n_global, zt = 64, 16
+    res = _launch("mim", n_global, kind)
+    sd = R.det_state("VAE", zt, 1)
+    _common_checks(res, sd)
+    for key in ("e0", "e1", "e3"):
+        assert np.array_equal(res[0][key], res[1][key]), key
+    hp = {"temperature": 0.1, "beta": 0.125, "loc": 0, "scale": 1, "alpha": 100.0, "lambda": 3.0}
+    x, label, ec, es, _ = R.det_inputs(n_global, 1, 28, zt, 4, seed=21)
+    gen = np.random.default_rng(5)
+    noises = [(ec, es)] + [(gen.standard_normal((n_global, zt // 2)), gen.standard_normal((n_global, zt // 2)))
+                           for _ in range(5)]
+    M0 = R.to_torch(R.det_mlp(zt // 2, zt))
+    shards = []
+    for r in (0, 1):
+        lo, hi = res[r]["bounds"]
+        o = R.mim_step(R.to_torch(sd), M0, torch.tensor(x[lo:hi]), torch.tensor(label[lo:hi]), torch.tensor(ec[lo:hi]),
+                       torch.tensor(es[lo:hi]), torch.tensor(res[r]["perm"]), "VAE", hp, kind)
+        shards.append(o)
+        got = res[r]["losses"]
+        for i, k in ((0, "rec"), (1, "kl_c"), (2, "kl_s"), (3, "c_loss"), (5, "mi")):
+            ref = float(o[k])
+            assert abs(float(got[i]) - ref) <= LOSS_TOL * max(abs(ref), 1e-2), (r, k, float(got[i]), ref)
+    mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
+    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, "VAE")
+    # the estimator: 5 x (per-shard train-mode forward with noise j on the updated VAE, per-shard
+    # learning-loss gradient, mean over shards, torch Adam)
+    P1 = R.to_torch(sd, requires_grad=False)
+    P1.update(_adam_ref(sd, mean_g))
+    Ps = [dict(P1), dict(P1)]
+    for P in Ps:  # each rank's BN buffers evolve on its own shard
+        for k in list(P):
+            if "running" in k or "num_batches" in k:
+                P[k] = P[k].clone()
+    mparams = [M0[k].detach().clone().requires_grad_(True) for k in M0]
+    Md = dict(zip(M0.keys(), mparams))
+    eopt = torch.optim.Adam(mparams, lr=2e-3)
+    for j in range(5):
+        a, b = noises[1 + j]
+        lls = []
+        grads = None
+        for r in (0, 1):
+            lo, hi = res[r]["bounds"]
+            with torch.no_grad():
+                _, _, zz = R.vae_forward(Ps[r], torch.tensor(x[lo:hi]), torch.tensor(a[lo:hi]), torch.tensor(b[lo:hi]),
+                                         "VAE", True)
+            ll = R.learning_loss(Md, zz[:, : zt // 2], zz[:, zt // 2:])
+            g = torch.autograd.grad(ll, mparams)
+            grads = [gi / 2 for gi in g] if grads is None else [acc + gi / 2 for acc, gi in zip(grads, g)]
+            lls.append(float(ll))
+            assert abs(float(res[r]["learn"][j]) - lls[-1]) <= 1e-4 * max(abs(lls[-1]), 1.0), (r, j)
+        for p_, g in zip(mparams, grads):
+            p_.grad = g
+        eopt.step()
+    # the estimator arena holds the parameters in est_params order (p_mu then p_logvar, weight, bias)
+    ref_e = torch.cat([Md[k].detach().reshape(-1) for k in ("p_mu.0.weight", "p_mu.0.bias", "p_mu.2.weight",
+                                                            "p_mu.2.bias", "p_logvar.0.weight", "p_logvar.0.bias",
+                                                            "p_logvar.2.weight", "p_logvar.2.bias")])
+    e1 = res[0]["e1"]
+    got_e = []
+    o = 0
+    for k in ("p_mu.0.weight", "p_mu.0.bias", "p_mu.2.weight", "p_mu.2.bias", "p_logvar.0.weight", "p_logvar.0.bias",
+              "p_logvar.2.weight", "p_logvar.2.bias"):
+        nel = Md[k].numel()
+        got_e.append(torch.tensor(e1[o:o + nel]))
+        o = (o + nel + 3) & ~3
+    assert _rel(torch.cat(got_e), ref_e) < 1e-3
