@@ -32,6 +32,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense FP32 (MFMA f32 = VALU rate), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (no sparsity), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
 CONFIGS = {
@@ -42,6 +43,10 @@ CONFIGS = {
                    dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, la=3.0, mi_lr=2e-3), "CLUBSample"),
     "celeba": ("VAE64", 64, 3, 64, 256, "clear", 4,
                dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, ps=True), None),
+    # configs[4]: Camelyon17 patches resized to 64x64 before the model, bs=1024 over 8 GPUs =
+    # 128 per GPU, bf16 contractions
+    "camelyon-bf16": ("VAE64", 64, 3, 64, 128, "clear", 2,
+                      dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, ps=True, precision="bf16"), None),
 }
 
 
@@ -52,11 +57,11 @@ def make_trainer(cfg, device):
     if mode == "clear":
         return get_clearvae_trainer(beta=hp["beta"], ps=hp["ps"], vae_lr=hp["vae_lr"], z_dim=z, alpha=hp["alpha"],
                                     temperature=hp["temperature"], device=device, vae_arch=arch, in_channel=C,
-                                    verbose_period=10**9)
+                                    verbose_period=10**9, precision=hp.get("precision", "fp32"))
     return get_clearmimvae_trainer(beta=hp["beta"], mi_estimator=est, la=hp["la"], vae_lr=hp["vae_lr"],
                                    mi_estimator_lr=hp["mi_lr"], z_dim=z, alpha=hp["alpha"],
                                    temperature=hp["temperature"], device=device, vae_arch=arch, in_channel=C,
-                                   verbose_period=10**9)
+                                   verbose_period=10**9, precision=hp.get("precision", "fp32"))
 
 
 def conv_flops_per_image(spec):
@@ -299,8 +304,9 @@ def main():
         if best is not None:
             label, ms, fl = best
             ach = fl / (ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "kernel": label, "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None,
+            peak = PEAK_BF16_TFLOPS if hp.get("precision") == "bf16" else PEAK_FP32_TFLOPS
+            roof = {"bound": "mfma", "kernel": label, "achieved": round(ach, 3), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
                     "kernel_ms": round(ms, 5), "flops_per_launch": fl}
             # HBM bytes per launch of the same call from the committed rocprofv3 PMC passes
             # (profiles/pmc_traffic.py), when they were taken on this call
@@ -337,7 +343,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": hp.get("precision", "fp32"),
             "data": "synthetic U[0,1) images, uniform labels, resident in HBM; deterministic random-init weights",
             "config": {"workload": f"{args.config}: CLEAR-{'VAE' if mode == 'clear' else 'MIM (CLUB-S)'} {arch} "
                                    f"z={z} {C}x{hw}x{hw} per-GPU bs={B}", "model": arch, "global_batch": world * B,

@@ -26,6 +26,13 @@ namespace cv {
 namespace fast {
 
 constexpr int LDK = BK + 4;  // LDS row pitch (floats) of both k-contiguous operand images
+// bf16 operand images (MT = MMA_BF16): the same [row][k] images with k-contiguous bf16 and an 80-byte
+// row pitch, so the 16 rows of a ds_read_b128 fragment start on 16 disjoint 4-bank groups
+constexpr int LDKH = BK + 8;
+enum { MMA_F32 = 0, MMA_BF16 = 1 };
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ bf16x4 to_bf16x4(f32x4 v) { return __builtin_convertvector(v, bf16x4); }
 
 __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ f32x4 g4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -159,7 +166,9 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
 #ifndef CV_FAST_MINW_64
 #define CV_FAST_MINW_64 1
 #endif
-template <int OP, int BM, int BN, int XA, int XB, int EPI, int D>
+// MT: MMA_F32 (v_mfma_f32_16x16x4_f32, fp32 operands) or MMA_BF16 (operands rounded to bf16 when
+// staged into LDS after the fp32 transform, v_mfma_f32_16x16x32_bf16, fp32 accumulation)
+template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
 __global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? CV_FAST_MINW_SMALL : (BM == 64 ? CV_FAST_MINW_64 : 1))
 void gemm_kernel(const Args P) {
   static_assert(D >= 2, "the register ring needs at least two stages (D=1 is not a valid schedule)");
@@ -177,6 +186,9 @@ void gemm_kernel(const Args P) {
   float* As = smem;                       // [2][BM][LDK]
   float* Bs = As + 2 * BM * LDK;          // [2][BN][LDK]
   float* red = Bs + 2 * BN * LDK;         // [2][WM][BN]
+  // bf16 images live at the start of the same regions ([2][BM][LDKH] / [2][BN][LDKH] halves)
+  __bf16* Ah = reinterpret_cast<__bf16*>(As);
+  __bf16* Bh = reinterpret_cast<__bf16*>(Bs);
   const bool bn1d = (OP == OP_DENSE) && XA != CV_XF_NONE && P.ca_n == P.K;
   const int nfa = (XA == CV_XF_NONE) ? 0 : (bn1d ? P.kchunk : P.ca_n);
   const int nfb = (XFB == CV_XF_NONE) ? 0 : P.cb_n;
@@ -452,6 +464,8 @@ void gemm_kernel(const Args P) {
   auto store = [&](Stage& S, int buf) {
     float* Ab = As + buf * BM * LDK;
     float* Bb = Bs + buf * BN * LDK;
+    __bf16* Abh = Ah + buf * BM * LDKH;
+    __bf16* Bbh = Bh + buf * BN * LDKH;
     if constexpr (ROWS) {
       if constexpr (XA != CV_XF_NONE && OP != OP_DENSE) {
         if (S.cb0 != xa_cb0) {  // wave-uniform: a new channel block
@@ -470,7 +484,8 @@ void gemm_kernel(const Args P) {
           if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[i], xa);
         }
         if (!((S.am >> i) & 1u)) v = zero4();
-        *reinterpret_cast<f32x4*>(Ab + (ar + 32 * i) * LDK + 4 * aq) = v;
+        if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Abh + (ar + 32 * i) * LDKH + 4 * aq) = to_bf16x4(v);
+        else *reinterpret_cast<f32x4*>(Ab + (ar + 32 * i) * LDK + 4 * aq) = v;
       }
     } else {
       constexpr int MQ = BM / 4;
@@ -482,8 +497,14 @@ void gemm_kernel(const Args P) {
         if constexpr (XA == CV_XF_BNRELU) v = apply_xc<XA>(v, v, xa);
         if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[e], xa);
         if (!((S.am >> e) & 1u)) v = zero4();
+        if constexpr (MT == MMA_BF16) {
+          const bf16x4 h = to_bf16x4(v);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Ab[(4 * mq + j) * LDK + kk] = v[j];
+          for (int j = 0; j < 4; ++j) Abh[(4 * mq + j) * LDKH + kk] = h[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Ab[(4 * mq + j) * LDK + kk] = v[j];
+        }
       }
     }
 #pragma unroll
@@ -493,7 +514,10 @@ void gemm_kernel(const Args P) {
       if constexpr (BKC) {
         const int n = idx >> 3, kq = idx & 7;
         if (!((S.bm >> e) & 1u)) v = zero4();
-        if (n < BN) *reinterpret_cast<f32x4*>(Bb + n * LDK + 4 * kq) = v;
+        if (n < BN) {
+          if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Bbh + n * LDKH + 4 * kq) = to_bf16x4(v);
+          else *reinterpret_cast<f32x4*>(Bb + n * LDK + 4 * kq) = v;
+        }
       } else {
         constexpr int NQ = BN / 4;
         const int nq = idx % NQ, kk = idx / NQ;
@@ -502,8 +526,14 @@ void gemm_kernel(const Args P) {
         if (!((S.bm >> e) & 1u)) v = zero4();
         if (OP == OP_WGRAD && ((S.bone >> e) & 1u)) v = f32x4{1.f, 0.f, 0.f, 0.f};
         if (kk < BK) {
+          if constexpr (MT == MMA_BF16) {
+            const bf16x4 h = to_bf16x4(v);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) Bb[(4 * nq + j) * LDK + kk] = v[j];
+            for (int j = 0; j < 4; ++j) Bbh[(4 * nq + j) * LDKH + kk] = h[j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Bb[(4 * nq + j) * LDK + kk] = v[j];
+          }
         }
       }
     }
@@ -633,6 +663,22 @@ void gemm_kernel(const Args P) {
 #if defined(CV_ABLATE) && CV_ABLATE == 1
     return;  // diagnostic build: no fragment reads / MFMAs
 #endif
+    if constexpr (MT == MMA_BF16) {
+      // lane l: A[row l&15][k = 8(l>>4) .. +7], B[k = 8(l>>4) .. +7][col l&15]; one MFMA per BK=32
+      static_assert(BK == 32, "one 16x16x32 step per K tile");
+      const __bf16* Ab = Ah + buf * BM * LDKH + (wm * TM + fr) * LDKH + 8 * (lane >> 4);
+      const __bf16* Bb = Bh + buf * BN * LDKH + (wn * TN + fr) * LDKH + 8 * (lane >> 4);
+      bf16x8 av[FM], bv[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDKH);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDKH);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      return;
+    }
     const float* Ab = Af + buf * BM * LDK;
     const float* Bb = Bf + buf * BN * LDK;
     f32x4 av[BK / 16][FM], bv[BK / 16][FN];
@@ -794,7 +840,7 @@ void gemm_kernel(const Args P) {
 #define CV_FAST_DEPTH 2
 #endif
 
-template <int OP, int BM, int BN, int XA, int XB, int EPI>
+template <int OP, int BM, int BN, int XA, int XB, int EPI, int MT>
 int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
   constexpr int XFB = (OP == OP_WGRAD) ? XB : CV_XF_NONE;
   const bool bn1d = (OP == OP_DENSE) && XA != CV_XF_NONE && a.ca_n == a.K;
@@ -809,7 +855,7 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
   constexpr int DEPTH = (XA == CV_XF_BNBWD && BM == 64 && BN <= 32) ? CV_FAST_DEPTH_BNBWD
                         : (OP == OP_WGRAD && BM == 128)            ? CV_FAST_DEPTH_WGRAD
                                                                    : CV_FAST_DEPTH;
-  auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, DEPTH>;
+  auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, DEPTH, MT>;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) {
@@ -833,29 +879,29 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
 }
 
 // dispatch over the transform / epilogue modes of one (op, tile)
-template <int OP, int BM, int BN>
+template <int OP, int BM, int BN, int MT>
 int dispatch_modes(const Args& a, int xb, dim3 grid, hipStream_t st) {
   const int xa = a.a.xf, ep = a.ep.stat_mode;
 #define CV_FAST_EP(XA_, XB_)                                                            \
-  if (ep == CV_STAT_NONE) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE>(a, grid, st); \
-  if (ep == CV_STAT_FWD) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_FWD>(a, grid, st);   \
-  return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_BWD>(a, grid, st);
+  if (ep == CV_STAT_NONE) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE, MT>(a, grid, st); \
+  if (ep == CV_STAT_FWD) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_FWD, MT>(a, grid, st);   \
+  return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_BWD, MT>(a, grid, st);
 #define CV_FAST_XA(XB_)                        \
   if (xa == CV_XF_NONE) { CV_FAST_EP(CV_XF_NONE, XB_) } \
   if (xa == CV_XF_BNRELU) { CV_FAST_EP(CV_XF_BNRELU, XB_) } \
   CV_FAST_EP(CV_XF_BNBWD, XB_)
   if constexpr (OP == OP_WGRAD) {  // no epilogue statistics; B transform
 #undef CV_FAST_EP
-#define CV_FAST_EP(XA_, XB_) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE>(a, grid, st);
+#define CV_FAST_EP(XA_, XB_) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE, MT>(a, grid, st);
     if (xb == CV_XF_NONE) { CV_FAST_XA(CV_XF_NONE) }
     if (xb == CV_XF_BNRELU) { CV_FAST_XA(CV_XF_BNRELU) }
     CV_FAST_XA(CV_XF_BNBWD)
   } else if constexpr (OP == OP_DENSE) {
 #undef CV_FAST_EP
 #define CV_FAST_EP(XA_, XB_)                                                            \
-  if (ep == CV_STAT_NONE) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE>(a, grid, st); \
-  if (ep == CV_STAT_FWD) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_FWD>(a, grid, st);   \
-  return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_BWD>(a, grid, st);
+  if (ep == CV_STAT_NONE) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_NONE, MT>(a, grid, st); \
+  if (ep == CV_STAT_FWD) return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_FWD, MT>(a, grid, st);   \
+  return launch_fast<OP, BM, BN, XA_, XB_, CV_STAT_BWD, MT>(a, grid, st);
     if (xb == DB_KCONT) { CV_FAST_XA(DB_KCONT) }
     if (xb == DB_NCONT) { CV_FAST_XA(DB_NCONT) }
     CV_FAST_XA(DB_KPERM)
@@ -866,15 +912,15 @@ int dispatch_modes(const Args& a, int xb, dim3 grid, hipStream_t st) {
 #undef CV_FAST_XA
 }
 
-template <int OP>
+template <int OP, int MT>
 int dispatch_tiles(const Args& a, int xb, int BM, int BN, dim3 grid, hipStream_t st) {
-  if (BM == 64 && BN == 16) return dispatch_modes<OP, 64, 16>(a, xb, grid, st);
-  if (BM == 64 && BN == 32) return dispatch_modes<OP, 64, 32>(a, xb, grid, st);
-  if (BM == 64 && BN == 64) return dispatch_modes<OP, 64, 64>(a, xb, grid, st);
+  if (BM == 64 && BN == 16) return dispatch_modes<OP, 64, 16, MT>(a, xb, grid, st);
+  if (BM == 64 && BN == 32) return dispatch_modes<OP, 64, 32, MT>(a, xb, grid, st);
+  if (BM == 64 && BN == 64) return dispatch_modes<OP, 64, 64, MT>(a, xb, grid, st);
   if constexpr (OP != OP_DENSE) {
-    if (BM == 128 && BN == 16) return dispatch_modes<OP, 128, 16>(a, xb, grid, st);
-    if (BM == 128 && BN == 32) return dispatch_modes<OP, 128, 32>(a, xb, grid, st);
-    if (BM == 128 && BN == 64) return dispatch_modes<OP, 128, 64>(a, xb, grid, st);
+    if (BM == 128 && BN == 16) return dispatch_modes<OP, 128, 16, MT>(a, xb, grid, st);
+    if (BM == 128 && BN == 32) return dispatch_modes<OP, 128, 32, MT>(a, xb, grid, st);
+    if (BM == 128 && BN == 64) return dispatch_modes<OP, 128, 64, MT>(a, xb, grid, st);
   }
   return -1;
 }

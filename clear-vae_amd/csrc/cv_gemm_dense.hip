@@ -18,7 +18,8 @@ int gemm_fast_dense(const Args& a, int BM, int BN, dim3 grid, hipStream_t st) {
   }
   // 32-bit element offsets in the kernel
   if ((long)a.M * a.lda >= (1L << 31) || (long)(a.wlayout ? a.K : a.N) * a.ldb >= (1L << 31)) return -1;
-  return fast::dispatch_tiles<OP_DENSE>(a, xb, BM, BN, grid, st);
+  if (a.mma == CV_MMA_BF16) return gemm_fast_dense_bf16(a, xb, BM, BN, grid, st);
+  return fast::dispatch_tiles<OP_DENSE, fast::MMA_F32>(a, xb, BM, BN, grid, st);
 }
 
 }  // namespace cv

@@ -9,7 +9,8 @@ int gemm_fast_gather(const Args& a, int BM, int BN, dim3 grid, hipStream_t st) {
   // 32-bit element offsets in the kernel
   if ((long)a.g.n * a.g.hb * a.g.wb * a.g.cb >= (1L << 31) || (long)a.g.n * a.g.hs * a.g.ws * a.g.cs >= (1L << 31))
     return -1;
-  return fast::dispatch_tiles<OP_GATHER>(a, 0, BM, BN, grid, st);
+  if (a.mma == CV_MMA_BF16) return gemm_fast_gather_bf16(a, BM, BN, grid, st);
+  return fast::dispatch_tiles<OP_GATHER, fast::MMA_F32>(a, 0, BM, BN, grid, st);
 }
 
 }  // namespace cv

@@ -960,6 +960,7 @@ static int check_conv(const cv_conv* g) {
   CV_REQUIRE(g && g->n > 0 && g->c_in > 0 && g->c_out > 0 && g->kh > 0 && g->kw > 0 && g->stride > 0 &&
                  g->pad >= 0,
              "conv: bad geometry");
+  CV_REQUIRE(g->mma == CV_MMA_FP32 || g->mma == CV_MMA_BF16, "conv: bad mma precision %d", g->mma);
   const cv_conv& c = *g;
   if (!c.transposed) {
     const int ho = (c.h_in + 2 * c.pad - c.kh) / c.stride + 1, wo = (c.w_in + 2 * c.pad - c.kw) / c.stride + 1;
@@ -975,7 +976,7 @@ static int check_conv(const cv_conv* g) {
 
 // GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
 static int run_gather(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
-                      const cv_epilogue* ep, hipStream_t st, const char* what) {
+                      const cv_epilogue* ep, hipStream_t st, const char* what, int mma) {
   if (!g_force_generic) {
     const int er = edge_gather(g, in, w, bias, out, ep, st);
     if (er >= 0) return er;
@@ -985,6 +986,7 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
   Args a;
   init_args(a);
   a.op = OP_GATHER;
+  a.mma = mma;
   a.g = g;
   a.a = *in;
   a.ca_n = (in->xf != CV_XF_NONE) ? g.cb : 0;
@@ -1004,7 +1006,7 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
 
 // SCATTER with big = rows. `in` is the small-grid tensor; w is packed [tap][cs][cb].
 static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
-                       const cv_epilogue* ep, hipStream_t st, const char* what) {
+                       const cv_epilogue* ep, hipStream_t st, const char* what, int mma) {
   if (!g_force_generic) {
     const int er = edge_scatter(g, in, w, bias, out, ep, st);
     if (er >= 0) return er;
@@ -1014,6 +1016,7 @@ static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const
   Args a;
   init_args(a);
   a.op = OP_SCATTER;
+  a.mma = mma;
   a.g = g;
   a.a = *in;
   a.ca_n = (in->xf != CV_XF_NONE) ? g.cs : 0;
@@ -1084,7 +1087,7 @@ int wgrad_reduce_launch(const float* part, int split, int M, int N, int ntot, in
 }
 
 static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias,
-                     int split_k, float* work, size_t work_bytes, hipStream_t st) {
+                     int split_k, float* work, size_t work_bytes, hipStream_t st, int mma) {
   if (split_k <= 0 && !g_force_generic) {
     const int er = edge_wgrad(g, small, big, gw, gbias, work, work_bytes, st);
     if (er >= 0) return er;
@@ -1092,6 +1095,7 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   Args a;
   init_args(a);
   a.op = OP_WGRAD;
+  a.mma = mma;
   a.g = g;
   a.a = *small;
   a.b = *big;
@@ -1189,8 +1193,8 @@ extern "C" int cv_conv_forward(const cv_conv* g, const cv_operand* in, const flo
   if (check_conv(g) || check_operand(in, "conv_forward")) return 1;
   CV_REQUIRE(wpacked && out, "conv_forward: null weight/out");
   const Geo geo = geo_of(g);
-  if (!g->transposed) return run_gather(geo, in, wpacked, bias, out, ep, S(stream), "conv_forward");
-  return run_scatter(geo, in, wpacked, bias, out, ep, S(stream), "convT_forward");
+  if (!g->transposed) return run_gather(geo, in, wpacked, bias, out, ep, S(stream), "conv_forward", g->mma);
+  return run_scatter(geo, in, wpacked, bias, out, ep, S(stream), "convT_forward", g->mma);
 }
 
 extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* wpacked, float* gin,
@@ -1199,8 +1203,9 @@ extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, c
   if (check_conv(g) || check_operand(gout, "conv_backward_data")) return 1;
   CV_REQUIRE(wpacked && gin, "conv_backward_data: null weight/gin");
   const Geo geo = geo_of(g);
-  if (!g->transposed) return run_scatter(geo, gout, wpacked, nullptr, gin, ep, S(stream), "conv_backward_data");
-  return run_gather(geo, gout, wpacked, nullptr, gin, ep, S(stream), "convT_backward_data");
+  if (!g->transposed)
+    return run_scatter(geo, gout, wpacked, nullptr, gin, ep, S(stream), "conv_backward_data", g->mma);
+  return run_gather(geo, gout, wpacked, nullptr, gin, ep, S(stream), "convT_backward_data", g->mma);
 }
 
 extern "C" size_t cv_conv_wgrad_workspace_bytes(const cv_conv* g, int split_k) {
@@ -1221,8 +1226,8 @@ extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, c
   const Geo geo = geo_of(g);
   CV_REQUIRE(!g->transposed || !gbias, "convT bias gradient is not a WGRAD column (use a reduction)");
   // conv: small = dY, big = X ; convT: small = X, big = dY
-  if (!g->transposed) return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream));
-  return run_wgrad(geo, in, gout, gweight, nullptr, split_k, work, work_bytes, S(stream));
+  if (!g->transposed) return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream), g->mma);
+  return run_wgrad(geo, in, gout, gweight, nullptr, split_k, work, work_bytes, S(stream), g->mma);
 }
 
 // ---------------------------------------------------------------- linear layers
@@ -1240,6 +1245,7 @@ extern "C" int cv_linear_forward(const cv_linear* g, const cv_operand* in, const
                                  float* out, int accumulate, const cv_epilogue* ep, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(g && g->n > 0 && g->in_features > 0 && g->out_features > 0, "linear_forward: bad geometry");
+  CV_REQUIRE(g->mma == CV_MMA_FP32 || g->mma == CV_MMA_BF16, "linear_forward: bad mma precision %d", g->mma);
   if (check_operand(in, "linear_forward")) return 1;
   CV_REQUIRE(weight && out, "linear_forward: null weight/out");
   const int ip = g->in_pix > 0 ? g->in_pix : 1, op = g->out_pix > 0 ? g->out_pix : 1;
@@ -1248,6 +1254,7 @@ extern "C" int cv_linear_forward(const cv_linear* g, const cv_operand* in, const
   Args a;
   init_args(a);
   a.op = OP_DENSE;
+  a.mma = g->mma;
   a.a = *in;
   if (in->xf != CV_XF_NONE) {
     a.ca_n = in->bn.C;
@@ -1276,6 +1283,7 @@ extern "C" int cv_linear_backward_data(const cv_linear* g, const cv_operand* gou
                                        int accumulate, const cv_epilogue* ep, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(g && g->n > 0 && g->in_features > 0 && g->out_features > 0, "linear_backward_data: bad geometry");
+  CV_REQUIRE(g->mma == CV_MMA_FP32 || g->mma == CV_MMA_BF16, "linear_backward_data: bad mma precision %d", g->mma);
   if (check_operand(gout, "linear_backward_data")) return 1;
   CV_REQUIRE(weight && gin, "linear_backward_data: null weight/gin");
   const int ip = g->in_pix > 0 ? g->in_pix : 1, op = g->out_pix > 0 ? g->out_pix : 1;
@@ -1283,6 +1291,7 @@ extern "C" int cv_linear_backward_data(const cv_linear* g, const cv_operand* gou
   Args a;
   init_args(a);
   a.op = OP_DENSE;
+  a.mma = g->mma;
   a.a = *gout;
   if (gout->xf != CV_XF_NONE) {
     a.ca_n = gout->bn.C;
@@ -1316,6 +1325,7 @@ extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* g
                                          cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(g && g->n > 0, "linear_backward_weight: bad geometry");
+  CV_REQUIRE(g->mma == CV_MMA_FP32 || g->mma == CV_MMA_BF16, "linear_backward_weight: bad mma precision %d", g->mma);
   if (check_operand(gout, "linear_backward_weight") || check_operand(in, "linear_backward_weight")) return 1;
   const int ip = g->in_pix > 0 ? g->in_pix : 1;
   CV_REQUIRE(g->out_pix <= 1, "linear_backward_weight: permuted outputs unsupported (use cv_declinear_*)");
@@ -1335,5 +1345,5 @@ extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* g
   }
   geo.s = 1;
   geo.p = 0;
-  return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream));
+  return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream), g->mma);
 }

@@ -46,6 +46,7 @@ struct Args {
   int lda, a_pix, a_ch;      // DENSE: A row stride; NCHW-flatten permutation of A columns (a_pix=1: none)
   int ldo, o_pix, o_ch;      // DENSE: out row stride; permutation of output columns
   int ca_n, cb_n, ce_n;      // feature counts of a / b / epilogue BN constants (0 = unused)
+  int mma;                   // CV_MMA_FP32 / CV_MMA_BF16 operand precision of the specialised core
   // fast divisors (filled by finalize_divs at launch)
   FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
 };
@@ -103,6 +104,11 @@ int gemm_fast_gather(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
 int gemm_fast_scatter(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
 int gemm_fast_wgrad(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
 int gemm_fast_dense(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
+// bf16-operand instances (cv_gemm_*_bf16.hip), called by the above when a.mma == CV_MMA_BF16
+int gemm_fast_gather_bf16(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
+int gemm_fast_scatter_bf16(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
+int gemm_fast_wgrad_bf16(const Args& a, int BM, int BN, dim3 grid, hipStream_t st);
+int gemm_fast_dense_bf16(const Args& a, int xb, int BM, int BN, dim3 grid, hipStream_t st);
 // occupancy query: while non-null, a gemm_fast_* call that would launch stores the chosen kernel's
 // resident workgroups per CU here instead (and launches nothing)
 extern thread_local int* g_fast_occ_query;

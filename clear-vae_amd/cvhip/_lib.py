@@ -32,6 +32,8 @@ XF_NONE, XF_BNRELU, XF_BNBWD = 0, 1, 2
 STAT_NONE, STAT_FWD, STAT_BWD = 0, 1, 2
 SIM = {"cosine": 0, "l2": 1, "modified_l2": 2, "jeffrey": 3, "mahalanobis": 4}
 MI_NONE, MI_CLUBSAMPLE, MI_L1OUT = 0, 1, 2
+MMA_FP32, MMA_BF16 = 0, 1  # CV_MMA_*
+PRECISION = {"fp32": MMA_FP32, "bf16": MMA_BF16}
 
 
 class cv_bn(ctypes.Structure):
@@ -81,6 +83,7 @@ class cv_conv(ctypes.Structure):
         ("stride", c_int),
         ("pad", c_int),
         ("transposed", c_int),
+        ("mma", c_int),
     ]
 
 
@@ -93,6 +96,7 @@ class cv_linear(ctypes.Structure):
         ("in_ch", c_int),
         ("out_pix", c_int),
         ("out_ch", c_int),
+        ("mma", c_int),
     ]
 
 

@@ -182,7 +182,8 @@ class ClearStep:
     # ----------------------------------------------------------------------------- bookkeeping
     def _signature(self):
         t = self.trainer
-        sig = (id(t.optimizer), t.sim_fn, tuple(sorted((k, str(v)) for k, v in t.hyperparameter.items())))
+        sig = (id(t.optimizer), t.sim_fn, tuple(sorted((k, str(v)) for k, v in t.hyperparameter.items())),
+               getattr(self.vae, "_cv_precision", "fp32"))
         if self.mode == "mim":
             sig += (id(t.mi_estimator), id(t.mi_estimator_optimizer))
         return sig

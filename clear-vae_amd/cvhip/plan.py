@@ -54,12 +54,13 @@ class ConvSpec:
     # GEMM-native weight copies (cv_pack_conv_weights): read by the forward / backward-data launch
     wfwd: object = None
     wbwd: object = None
+    mma: int = 0  # CV_MMA_* operand precision of this layer's GEMMs (cvhip.set_precision)
 
     def geom(self, n: int) -> cv_conv:
         m = self.mod
         return cv_conv(
             n, self.c_in, self.h_in, self.w_in, self.c_out, self.h_out, self.w_out,
-            m.kernel_size[0], m.kernel_size[1], m.stride[0], m.padding[0], int(self.transposed),
+            m.kernel_size[0], m.kernel_size[1], m.stride[0], m.padding[0], int(self.transposed), self.mma,
         )
 
 
@@ -76,6 +77,7 @@ class VaeSpec:
     dec_bn: nn.BatchNorm1d
     unflat: tuple  # (C, H, W) of the decoder Linear output
     dec: list = field(default_factory=list)
+    mma: int = 0  # CV_MMA_* of the linear layers (the convs carry their own, set together)
 
     @property
     def F(self) -> int:
@@ -235,7 +237,30 @@ def ensure_arena(vae: nn.Module, spec_fn=None):
     vae._cv_arena = arena
     vae._cv_spec = spec
     vae._cv_workspaces = {}
+    _apply_precision(spec, getattr(vae, "_cv_precision", "fp32"))
     return arena
+
+
+def _apply_precision(spec: VaeSpec, precision: str):
+    if precision not in _lib.PRECISION:
+        raise ValueError(f"precision must be one of {sorted(_lib.PRECISION)}, got {precision!r}")
+    mma = _lib.PRECISION[precision]
+    spec.mma = mma
+    for c in spec.enc + spec.dec:
+        c.mma = mma
+
+
+def set_precision(vae: nn.Module, precision: str = "fp32"):
+    """Operand precision of the model's conv / linear contractions on the HIP path: "fp32" (the
+    reference's arithmetic, default) or "bf16" (BASELINE configs[4]: operands rounded to bf16 for
+    v_mfma_f32_16x16x32_bf16, fp32 accumulation; activations, BatchNorm statistics, losses and Adam stay
+    fp32).  Takes effect at the next step: a fused engine built for the other precision rebuilds."""
+    if precision not in _lib.PRECISION:
+        raise ValueError(f"precision must be one of {sorted(_lib.PRECISION)}, got {precision!r}")
+    vae._cv_precision = precision
+    spec = getattr(vae, "_cv_spec", None)
+    if spec is not None:
+        _apply_precision(spec, precision)
 
 
 def attach_packed(spec: VaeSpec, device):
@@ -544,7 +569,7 @@ class Workspace:
             cur = self.y_enc[li]
         # heads (Linear on the NCHW-flattened activation), split-K into a zeroed buffer
         C, Hh, Wh = sp.feat
-        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
+        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
         if zero_heads:  # (else the caller zeroed it earlier in the same program)
             P.add("cv_zero", self.heads, self.heads.numel() * 4)
         P.add("cv_linear_forward", lin, operand(cur, XF_BNRELU, self.bn_enc[-1].cv(train)),
@@ -565,7 +590,7 @@ class Workspace:
     def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None):
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
-        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
+        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
         ep = ep_fwd(self.bn_1d) if train else ep_none()
         P.add("cv_linear_forward", lin, operand(z), sp.dec_lin.weight, sp.dec_lin.bias, self.h, 0, ep)
         P.add("cv_bn_apply", self.bn_1d.cv(train), self.h, self.ah, n, sp.dec_lin.out_features, Hu * Wu, Cu, 1)
@@ -604,7 +629,7 @@ class Workspace:
             P.add_side("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
                        self.wg_bytes)
         Cu, Hu, Wu = sp.unflat
-        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu)
+        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
         P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
               self.z, param_grad(sp.dec_lin.weight))
         if zero_dz:  # (else the caller zeroed it earlier in the step)
@@ -616,7 +641,7 @@ class Workspace:
         """From d(heads) [n, 4d] to the encoder / heads parameter gradients (and dx if asked)."""
         sp, n = self.spec, self.n
         C, Hh, Wh = sp.feat
-        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0)
+        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
         a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
         P.add_side("cv_linear_backward_weight", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
                    param_grad(sp.heads[0].bias), 0, self.wg_work, self.wg_bytes)

@@ -7,6 +7,8 @@ accepts the same strings ("VAE", "VAE64", "CLUBSample", "L1OutUB", the CNN class
 import torch
 import torch.nn as nn
 
+from cvhip.plan import set_precision
+
 from src.models.cnn import LAMCNN64Classifier, LAMCNNClassifier, SimpleCNN64Classifier, SimpleCNNClassifier
 from src.models.mi_estimator import CLUB, CLUBMean, CLUBSample, InfoNCE, L1OutUB, VarUB
 from src.models.vae import VAE, VAE64
@@ -58,9 +60,11 @@ def get_hierarchical_vae_trainer(beta, vae_lr, z_dim, group_mode, device, vae_ar
 
 
 def get_clearvae_trainer(beta, ps, vae_lr, z_dim, alpha, temperature, device, vae_arch: str = "VAE",
-                         in_channel: int = 1, verbose_period: int = 5):
-    """(trainer_utils.py:87-116)"""
+                         in_channel: int = 1, verbose_period: int = 5, precision: str = "fp32"):
+    """(trainer_utils.py:87-116).  `precision` (not in the reference, default its fp32): "bf16" runs the
+    conv / linear contractions on bf16 MFMA operands (cvhip.plan.set_precision)."""
     vae = _resolve(vae_arch)(total_z_dim=z_dim, in_channel=in_channel).to(device)
+    set_precision(vae, precision)
     optimizer = torch.optim.Adam(vae.parameters(), lr=vae_lr)
     return CLEARVAETrainer(
         vae, optimizer, sim_fn="cosine",
@@ -84,9 +88,11 @@ def get_cleartcvae_trainer(beta, la, vae_lr, factor_cls_lr, z_dim, alpha, temper
 
 
 def get_clearmimvae_trainer(beta, mi_estimator: str, la, vae_lr, mi_estimator_lr, z_dim, alpha, temperature,
-                            device, vae_arch: str = "VAE", in_channel: int = 1, verbose_period: int = 5):
-    """(trainer_utils.py:160-201)"""
+                            device, vae_arch: str = "VAE", in_channel: int = 1, verbose_period: int = 5,
+                            precision: str = "fp32"):
+    """(trainer_utils.py:160-201); `precision` as in get_clearvae_trainer."""
     vae = _resolve(vae_arch)(total_z_dim=z_dim, in_channel=in_channel).to(device)
+    set_precision(vae, precision)
     est = _resolve(mi_estimator)(x_dim=z_dim // 2, y_dim=z_dim // 2, hidden_size=z_dim).to(device)
     vae_opt = torch.optim.Adam(vae.parameters(), lr=vae_lr)
     est_opt = torch.optim.Adam(est.parameters(), lr=mi_estimator_lr)

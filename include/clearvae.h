@@ -95,6 +95,13 @@ typedef struct cv_epilogue {
   int erelu;          /* STAT_BWD: 1 if ReLU follows that BN                        */
 } cv_epilogue;
 
+/* Operand precision of a conv / linear contraction.  CV_MMA_BF16 (BASELINE configs[4], "bf16"): the
+ * specialised MFMA core rounds both operands to bf16 as it stages them into LDS (after the fp32 BatchNorm
+ * transform) and contracts on v_mfma_f32_16x16x32_bf16 with fp32 accumulation; activations, BatchNorm
+ * statistics and epilogues stay fp32.  Calls the core does not serve (image-facing edge layers) stay
+ * fp32.  The reference is fp32 only (CV_MMA_FP32, the default). */
+enum { CV_MMA_FP32 = 0, CV_MMA_BF16 = 1 };
+
 /* ---- convolution geometry (nn.Conv2d / nn.ConvTranspose2d, vae.py:15-46, 113-156) ---- */
 typedef struct cv_conv {
   int n;                          /* batch                                         */
@@ -102,6 +109,7 @@ typedef struct cv_conv {
   int c_out, h_out, w_out;        /* layer output (NHWC)                           */
   int kh, kw, stride, pad;
   int transposed;                 /* 0 Conv2d, 1 ConvTranspose2d                   */
+  int mma;                        /* CV_MMA_*: operand precision of the contraction */
 } cv_conv;
 
 /* GEMM-native copies of a conv / convT weight, refreshed once per optimizer step.  With
@@ -145,6 +153,7 @@ typedef struct cv_linear {
   int in_features, out_features;
   int in_pix, in_ch;   /* in_features = in_pix*in_ch, or in_pix = 1 for a plain row-major input   */
   int out_pix, out_ch; /* same for the output                                                      */
+  int mma;             /* CV_MMA_*                                                                  */
 } cv_linear;
 
 int cv_linear_forward(const cv_linear* g, const cv_operand* in, const float* weight,
