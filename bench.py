@@ -6,14 +6,22 @@ labels, CLEAR-VAE (VAE, z=16, beta=1/8, lr 5e-4, alpha=100, tau=0.1, ps=True,
 code/run_styledmnist_downstream_expr.py:231-238), fp32, one fused HIP training step per batch
 (forward, ELBO, 2 contrastive terms, backward, Adam) through CLEARVAETrainer's engine.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|celeba-mim|celeba]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|celeba-mim|celeba|camelyon-bf16]
 
 For N > 1 launch with torch.distributed.run (one process per GPU, RCCL): per-GPU batch fixed
 (weak scaling); value = images processed by all ranks / max-over-ranks wall time.
-After the timed region: (1) a per-kernel HIP-event pass over the same step program to price the
-dominant kernel against its roofline, (2) on rank 0 the CPU baseline (oracle/cpu_ref.py, the
-reference's math on torch-CPU) on a bounded sample, plus the ELBO relative error of one HIP step
-against the fp64 CPU reference on the same batch / weights / noise.
+
+After the timed region (nothing below is inside it):
+  (1) an in-step pass: the step's programs are enqueued eagerly behind a spin kernel long enough for the
+      host to queue the whole step, with a HIP timing-event pair around every call on the stream that call
+      runs on (the main or the weight-gradient side stream), so each call's time is its duration inside a
+      real step, concurrency included; the roofline is priced on the GEMM call with the largest in-step
+      time (`roofline.kernel`), with HBM `traffic` from the committed rocprofv3 PMC passes of that call;
+  (2) on rank 0 at N=1: the CPU baseline (oracle/ref_loop.py, the reference's step composition on
+      torch-CPU) on a bounded sample, and the ELBO (and, for CLEAR-MIM, MI) error of one HIP step against
+      the fp64 CPU reference on the same batch / weights / noise;
+  (3) default config at N=1: configs[2] (CelebA 64x64 bs=256 CLEAR-MIM CLUB-S) is timed the same way
+      and reported under "c3".
 """
 
 from __future__ import annotations
@@ -64,8 +72,8 @@ def make_trainer(cfg, device):
                                    verbose_period=10**9, precision=hp.get("precision", "fp32"))
 
 
-def conv_flops_per_image(spec):
-    """Algorithmic FLOPs of one training step per image (MAC x 2; fwd + bwd-data + bwd-weight)."""
+def layer_flops(spec):
+    """Algorithmic FLOPs of one forward pass per image (conv / linear MAC x 2)."""
     f = 0
     for c in spec.enc + spec.dec:
         k = c.mod.kernel_size[0] * c.mod.kernel_size[1]
@@ -75,16 +83,16 @@ def conv_flops_per_image(spec):
             macs = c.h_out * c.w_out * c.c_out * c.c_in * k
         f += 2 * macs
     f += 2 * spec.F * 4 * spec.d + 2 * 2 * spec.d * spec.dec_lin.out_features
-    return 3 * f
+    return f
 
 
-def kernel_pass(engine, G, reps=20, rounds=3):
-    """Per-call device time of the step program: each C-ABI call is captured REPS times back to back
-    into its own HIP graph (torch.cuda.CUDAGraph on the stream the kernels are launched on) and the
-    graph replay is bracketed by HIP events, so the average excludes host launch gaps.  Returns
-    {call label: mean ms per launch}.  (Repeating a call perturbs the workspace; run after timing.)"""
-    from cvhip import _lib
+def step_flops_per_image(spec, mode):
+    """training = 3x forward; CLEAR-MIM adds 5 forward-only passes."""
+    f = layer_flops(spec)
+    return 3 * f + (5 * f if mode == "mim" else 0)
 
+
+def _programs(G):
     progs = [("fwd", G["fwd"]), ("dec", G["dec"]), ("lat", G["lat"]), ("enc", G["enc"]), ("upd", G["upd"])]
     learn = G.get("learn")
     if isinstance(learn, list):  # data-parallel CLEAR-MIM: (gradient, Adam) program pairs
@@ -92,8 +100,52 @@ def kernel_pass(engine, G, reps=20, rounds=3):
             progs += [(f"learn{j}g", gp), (f"learn{j}a", ap)]
     elif learn is not None:
         progs.append(("learn", learn))
+    return progs
+
+
+def instep_pass(engine, G, rounds=6):
+    """In-step device time of every call of the step program (see the module docstring): returns
+    {label: mean ms per step} over `rounds` instrumented eager steps (a first one is discarded)."""
+    names = {id(P): name for name, P in _programs(G)}
+    segs = engine._segments(G, False)
+    ncalls = sum(len(P.calls) for item in segs if item[0] == "prog" for P in item[1])
+    acc, cnt = {}, 0
+    for r in range(rounds + 1):
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(ncalls * 200_000))  # ~80 us of queue per call at ~2.4 GHz
+        timers = []
+        for item in segs:
+            if item[0] == "prog":
+                for P in item[1]:
+                    t = []
+                    P.run(timer=t)
+                    timers.append((names[id(P)], P, t))
+            elif item[0] == "ar":
+                engine.buckets.launch(item[1])
+            elif item[0] == "wait":
+                engine.buckets.wait()
+            elif item[0] == "ar_est":
+                engine.est_buckets.launch(0)
+            elif item[0] == "wait_est":
+                engine.est_buckets.wait()
+        torch.cuda.synchronize()
+        if r == 0:
+            continue
+        cnt += 1
+        for pname, P, t in timers:
+            for i, e0, e1 in t:
+                lab = f"{pname}[{i}]:{P.calls[i][0]}"
+                acc[lab] = acc.get(lab, 0.0) + e0.elapsed_time(e1)
+    return {k: v / cnt for k, v in acc.items()}
+
+
+def isolated_pass(G, reps=20, rounds=3):
+    """Per-call device time in isolation: each call captured REPS times back to back into its own HIP
+    graph, replayed between HIP events.  (Repeating a call perturbs the workspace; run after timing.)"""
+    from cvhip import _lib
+
     times = {}
-    for pname, P in progs:
+    for pname, P in _programs(G):
         for i, (name, fn, args, _lane) in enumerate(P.calls):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -117,14 +169,15 @@ def kernel_pass(engine, G, reps=20, rounds=3):
     return times
 
 
-def gemm_flops_of(label, G, engine):
-    """Algorithmic FLOPs of one igemm call from its program position (conv / linear layers)."""
+def gemm_flops_of(label, G):
+    """Algorithmic FLOPs of one conv / linear call from its program position (None for other calls)."""
     pname, rest = label.split("[", 1)
     idx = int(rest.split("]")[0])
-    if not hasattr(G.get(pname), "calls"):
+    P = dict(_programs(G)).get(pname)
+    if P is None:
         return None
-    name, fn, args, _lane = G[pname].calls[idx]
-    if name.startswith("cv_conv_"):
+    name, fn, args, _lane = P.calls[idx]
+    if name in ("cv_conv_forward", "cv_conv_backward_data", "cv_conv_backward_weight"):
         g = args[0]._obj
         k = g.kh * g.kw
         if g.transposed:
@@ -132,56 +185,135 @@ def gemm_flops_of(label, G, engine):
         else:
             macs = g.n * g.h_out * g.w_out * g.c_out * g.c_in * k
         return 2.0 * macs
-    if name.startswith("cv_linear_"):
+    if name in ("cv_linear_forward", "cv_linear_backward_data", "cv_linear_backward_weight"):
         g = args[0]._obj
         return 2.0 * g.n * g.in_features * g.out_features
     return None
 
 
-def cpu_baseline(cfg, steps_budget_s=15.0):
-    """Reference math on the host (oracle/cpu_ref.py, torch-CPU fp32) on a bounded sample."""
-    import numpy as np
+def prefix_times(engine, G, labels, reps=20, rounds=3):
+    """In-graph, in-step duration of the given calls: a graph of the step's calls up to and including call
+    i, minus one up to call i-1, each replayed REPS times between HIP events on the launch stream (min of
+    ROUNDS).  Single-stream steps only (the default schedule); mutates the workspace (run after timing)."""
+    from cvhip.plan import Program
 
-    from oracle import cpu_ref as R
+    flat = []  # (label, call) in step order
+    for pname, P in _programs(G):
+        for i, c in enumerate(P.calls):
+            flat.append((f"{pname}[{i}]:{c[0]}", c))
+    if any(c[3] for _, c in flat):
+        return {}
+    pos = {lab: k for k, (lab, _) in enumerate(flat)}
+
+    def t_prefix(k):
+        if k < 0:
+            return 0.0
+        P = Program()
+        P.calls = [c for _, c in flat[:k + 1]]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            P.run()
+        g.replay()
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            best = ms if best is None else min(best, ms)
+        del g
+        return best
+
+    out = {}
+    for lab in labels:
+        k = pos[lab]
+        out[lab] = t_prefix(k) - t_prefix(k - 1)
+    return out
+
+
+def roofline_of(config, G, instep, precision, engine=None):
+    """Roofline of the GEMM call with the largest in-step time.  Candidates are ranked by the eager
+    in-step pass (whose event pairs add a few us per call); the top three are then re-timed inside a
+    replayed graph of the step by prefix differences (prefix_times), and the largest wins."""
+    cands = []
+    for label, ms in instep.items():
+        fl = gemm_flops_of(label, G)
+        if fl is not None:
+            cands.append((ms, label, fl))
+    if not cands:
+        return None
+    cands.sort(reverse=True)
+    timing = "in-step HIP events on the call's stream (eager, event pairs per call)"
+    if engine is not None:
+        pt = prefix_times(engine, G, [lab for _, lab, _ in cands[:3]])
+        if pt:
+            cands = sorted(((pt[lab], lab, fl) for _, lab, fl in cands[:3]), reverse=True)
+            timing = "in-step, replayed step graph: t(prefix through the call) - t(prefix before it)"
+    ms, label, fl = cands[0]
+    best = (label, ms, fl)
+    label, ms, fl = best
+    ach = fl / (ms * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if precision == "bf16" else PEAK_FP32_TFLOPS
+    roof = {"bound": "mfma", "kernel": label, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": None, "kernel_ms": round(ms, 5), "flops_per_launch": fl,
+            "timing": timing}
+    # HBM bytes per launch of the same call from the committed rocprofv3 PMC passes
+    # (profiles/pmc_traffic.py), when they were taken on this call
+    tpath = os.path.join(ROOT, "profiles", f"{config}_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            t = json.load(open(tpath))["calls"].get(label.split(":")[0])
+            if t is not None:
+                roof["traffic"] = round(float(t["traffic_bytes"]))
+        except (OSError, ValueError, KeyError):
+            pass
+    return roof
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, budget_s=15.0):
+    """The reference's training loop composition on the host cores (oracle/ref_loop.py, torch-CPU fp32),
+    on a bounded sample of the same workload."""
+    from oracle.ref_loop import RefLoop
 
     arch, z, C, hw, B, mode, nl, hp, est = cfg
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-    sd = R.det_state(arch, z, C)
-    P = R.to_torch(sd, torch.float32)
-    params = [v for v in P.values() if isinstance(v, torch.Tensor) and v.requires_grad]
-    opt = torch.optim.Adam(params, lr=hp["vae_lr"])
-    hpp = dict(temperature=hp["temperature"], alpha=hp["alpha"], beta=hp["beta"], ps=hp.get("ps", True),
-               **({"lambda": hp["la"]} if mode == "mim" else {}))
-    M = R.to_torch(R.det_mlp(z // 2, z), torch.float32) if mode == "mim" else None
-    steps = 0
-    work = 0.0
-    t0 = time.perf_counter()
-    while True:
-        x, label, ec, es, perm = R.det_inputs(B, C, hw, z, nl, seed=1000 + steps)
-        xt, lt = torch.tensor(x, dtype=torch.float32), torch.tensor(label)
-        ect, est_ = torch.tensor(ec, dtype=torch.float32), torch.tensor(es, dtype=torch.float32)
-        t_s = time.perf_counter()
-        if mode == "clear":
-            o = R.clear_step(P, xt, lt, ect, est_, arch, hpp, step=steps)
-        else:
-            o = R.mim_step(P, M, xt, lt, ect, est_, torch.tensor(perm), arch, hpp, step=steps)
-        for p, g in zip(params, o["grads"].values()):
-            p.grad = g
-        opt.step()
-        if mode == "mim":  # the 5 estimator updates each need a VAE forward (trainer.py:874-888)
-            with torch.no_grad():
-                for _ in range(5):
-                    R.vae_forward(P, xt, ect, est_, arch, True)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    loop = RefLoop(arch, z, C, mode, dict(hp))
+    g = torch.Generator().manual_seed(1000)
+    data = [(torch.rand(B, C, hw, hw, generator=g), torch.randint(0, nl, (B,), generator=g)) for _ in range(4)]
+    loop.step(*data[0])  # warm-up (allocator, oneDNN primitives)
+    steps, work = 0, 0.0
+    while work < budget_s and steps < 400:
+        X, y = data[steps % len(data)]
+        t0 = time.perf_counter()
+        loop.step(X, y)
+        work += time.perf_counter() - t0
         steps += 1
-        work += time.perf_counter() - t_s
-        if time.perf_counter() - t0 > steps_budget_s or steps >= 200:
-            break
     return {"value": round(B * steps / work, 1), "unit": "images/s", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"{steps} steps x bs={B} {arch} {mode} fp32 (oracle/cpu_ref.py + torch Adam)"}
+            "cpu_model": cpu_model(), "kind": "port",
+            "sample": f"{steps} steps x bs={B} {arch} {'CLEAR-VAE' if mode == 'clear' else 'CLEAR-MIM CLUB-S'} fp32: "
+                      "oracle/ref_loop.py, the reference's module/loss/trainer step composition on torch-CPU "
+                      "(within 1% of the reference's own CLEARVAETrainer._train in the dev container, DESIGN 7)"}
 
 
-def elbo_rel_err(cfg, device):
-    """One fused HIP step on a fixed batch with injected noise vs the fp64 CPU reference."""
+def step_error(cfg, device):
+    """One fused HIP step on a fixed batch with injected noise (and CLUB-S permutation) vs the fp64 CPU
+    reference: relative ELBO error (rec + w*KL_c + w*KL_s) and, for CLEAR-MIM, the MI error with an
+    absolute floor (|d| / max(|mi|, 1))."""
     import numpy as np
 
     from cvhip import rng
@@ -189,24 +321,110 @@ def elbo_rel_err(cfg, device):
     from oracle import cpu_ref as R
 
     arch, z, C, hw, B, mode, nl, hp, est = cfg
-    if mode != "clear":
-        return None
     tr = make_trainer(cfg, device)
     sd = R.det_state(arch, z, C)
     tr.model.load_state_dict({k: torch.as_tensor(np.asarray(v)).float() if np.asarray(v).dtype != np.int64
                               else torch.as_tensor(np.asarray(v)) for k, v in sd.items()})
-    eng = ClearStep.build(tr, "clear")
     x, label, ec, es, perm = R.det_inputs(B, C, hw, z, nl, seed=77)
     rng.clear_injections()
-    rng.inject_noise([torch.tensor(ec, dtype=torch.float32), torch.tensor(es, dtype=torch.float32)])
-    L = eng.step(torch.tensor(x, dtype=torch.float32, device=device), torch.tensor(label, device=device)).cpu()
-    hpp = dict(temperature=hp["temperature"], alpha=hp["alpha"], beta=hp["beta"], ps=hp["ps"])
-    o = R.clear_step(R.to_torch(sd), torch.tensor(x), torch.tensor(label), torch.tensor(ec), torch.tensor(es), arch,
-                     hpp)
+    X = torch.tensor(x, dtype=torch.float32, device=device)
+    L = torch.tensor(label, device=device)
     w = R.anneal_weight(0, hp["beta"])
-    elbo_hip = float(L[0]) + w * float(L[1]) + w * float(L[2])
-    elbo_ref = float(o["rec"]) + w * float(o["kl_c"]) + w * float(o["kl_s"])
-    return abs(elbo_hip - elbo_ref) / abs(elbo_ref)
+    if mode == "clear":
+        eng = ClearStep.build(tr, "clear")
+        rng.inject_noise([torch.tensor(ec, dtype=torch.float32), torch.tensor(es, dtype=torch.float32)])
+        Lh = eng.step(X, L).cpu()
+        hpp = dict(temperature=hp["temperature"], alpha=hp["alpha"], beta=hp["beta"], ps=hp["ps"])
+        o = R.clear_step(R.to_torch(sd), torch.tensor(x), torch.tensor(label), torch.tensor(ec), torch.tensor(es),
+                         arch, hpp)
+        out = {}
+    else:
+        M = R.det_mlp(z // 2, z)
+        tr.mi_estimator.load_state_dict({k: torch.tensor(v, dtype=torch.float32) for k, v in M.items()})
+        eng = ClearStep.build(tr, "mim")
+        gen = np.random.default_rng(5)
+        noise = [ec, es] + [gen.standard_normal((B, z // 2)) for _ in range(10)]
+        rng.inject_noise([torch.tensor(a, dtype=torch.float32) for a in noise])
+        rng.inject_perm([torch.tensor(perm)])
+        Lh, _ = eng.step(X, L)
+        Lh = Lh.cpu()
+        hpp = dict(temperature=hp["temperature"], alpha=hp["alpha"], beta=hp["beta"], **{"lambda": hp["la"]})
+        o = R.mim_step(R.to_torch(sd), R.to_torch(M), torch.tensor(x), torch.tensor(label), torch.tensor(ec),
+                       torch.tensor(es), torch.tensor(perm), arch, hpp, est)
+        mi_ref = float(o["mi"].detach())
+        out = {"mi_abs_err": abs(float(Lh[5]) - mi_ref), "mi_rel_err": abs(float(Lh[5]) - mi_ref) / max(abs(mi_ref), 1.0)}
+    elbo_hip = float(Lh[0]) + w * float(Lh[1]) + w * float(Lh[2])
+    elbo_ref = float(o["rec"].detach()) + w * float(o["kl_c"].detach()) + w * float(o["kl_s"].detach())
+    out["elbo_rel_err"] = abs(elbo_hip - elbo_ref) / abs(elbo_ref)
+    return out
+
+
+def run_workload(name, cfg, steps, warmup, device, world, rank, detail=True, kernel_table=None):
+    """Time `steps` fused steps of configuration `cfg` (after `warmup`), then the in-step pass."""
+    from cvhip.engine import ClearStep
+
+    arch, z, C, hw, B, mode, nl, hp, est = cfg
+    torch.manual_seed(0)
+    tr = make_trainer(cfg, device)
+    eng = ClearStep.build(tr, mode)
+    assert eng is not None, "fused engine unavailable"
+    # synthetic batches resident in HBM before timing (distinct per rank)
+    g = torch.Generator(device=device).manual_seed(1000 + rank)
+    nb = 8
+    Xs = [torch.rand(B, C, hw, hw, generator=g, device=device) for _ in range(nb)]
+    Ls = [torch.randint(0, nl, (B,), generator=g, device=device) for _ in range(nb)]
+
+    def step(i):
+        out = eng.step(Xs[i % nb], Ls[i % nb])
+        tr.annealer.step()
+        return out
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    finite = bool(torch.isfinite(eng.last_workspace(B).losses[:4]).all())
+    eng.sync_host_state()
+    value = world * B * steps / max(el, 1e-12)
+    res = {"value": value, "el": el, "ms_per_step": el / max(steps, 1) * 1e3, "finite": finite, "eng": eng,
+           "algorithmic_tflops": step_flops_per_image(eng.spec, mode) * value / 1e12}
+    if detail:
+        G = eng.graphs[B]
+        instep = instep_pass(eng, G)
+        res["instep"] = instep
+        res["roofline"] = roofline_of(name, G, instep, hp.get("precision", "fp32"), eng if world == 1 else None)
+        res["instep_sum_ms"] = sum(instep.values())
+        if kernel_table and rank == 0:
+            iso = isolated_pass(G)
+            with open(kernel_table, "w") as fh:
+                fh.write(f"{'call':60s} {'in-step ms':>11s} {'isolated':>9s} {'GFLOP':>8s} {'TF/s in-step':>12s}\n")
+                for label, ms in sorted(instep.items(), key=lambda kv: -kv[1]):
+                    fl = gemm_flops_of(label, G) or 0
+                    fh.write(f"{label:60s} {ms:11.4f} {iso.get(label, 0):9.4f} {fl / 1e9:8.3f} "
+                             f"{fl / (ms * 1e-3) / 1e12:12.2f}\n")
+                fh.write(f"{'total (sum of calls)':60s} {sum(instep.values()):11.4f} {sum(iso.values()):9.4f}\n")
+    return res
+
+
+def workload_label(name, cfg, world):
+    arch, z, C, hw, B, mode, nl, hp, est = cfg
+    kind = "CLEAR-VAE" if mode == "clear" else "CLEAR-MIM (CLUB-S)"
+    return {"workload": f"{name}: {kind} {arch} z={z} {C}x{hw}x{hw} per-GPU bs={B} {hp.get('precision', 'fp32')}",
+            "model": arch, "global_batch": world * B, "seq_len": None, "parallelism": f"dp{world}"}
 
 
 def main():
@@ -217,7 +435,8 @@ def main():
     ap.add_argument("--config", default="mnist", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-pass", action="store_true")
+    ap.add_argument("--no-kernel-pass", action="store_true", help="skip the in-step pass (profiling runs)")
+    ap.add_argument("--no-c3", action="store_true", help="default config: skip the configs[2] extra keys")
     ap.add_argument("--kernel-table", default=None, help="write the per-call timing table to this file")
     ap.add_argument("--only-call", default=None,
                     help="profiling mode: after warmup, launch this step-program call (e.g. 'enc[4]') --reps "
@@ -239,129 +458,68 @@ def main():
     cfg = tuple(cfg)
     arch, z, C, hw, B, mode, nl, hp, est = cfg
 
-    torch.manual_seed(0)
-    tr = make_trainer(cfg, device)
-    from cvhip.engine import ClearStep
-
-    eng = ClearStep.build(tr, mode)
-    assert eng is not None, "fused engine unavailable"
-    # synthetic batches resident in HBM before timing (distinct per rank)
-    g = torch.Generator(device=device).manual_seed(1000 + rank)
-    nb = 8
-    Xs = [torch.rand(B, C, hw, hw, generator=g, device=device) for _ in range(nb)]
-    Ls = [torch.randint(0, nl, (B,), generator=g, device=device) for _ in range(nb)]
-
-    def step(i):
-        out = eng.step(Xs[i % nb], Ls[i % nb])
-        tr.annealer.step()
-        return out
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
     if args.only_call:
         from cvhip import _lib
 
-        G = eng.graphs[B]
+        res = run_workload(args.config, cfg, 0, args.warmup, device, world, rank, detail=False)
+        G = res["eng"].graphs[B]
         pname, idx = args.only_call.split("[")
-        name, fn, cargs, _lane = G[pname].calls[int(idx.rstrip("]"))]
+        name, fn, cargs, _lane = dict(_programs(G))[pname].calls[int(idx.rstrip("]"))]
         s_ = _lib.stream_handle()
         for _ in range(args.reps):
             _lib.check(fn(*cargs, s_), name)
         torch.cuda.synchronize()
         print(json.dumps({"only_call": args.only_call, "name": name, "reps": args.reps}))
         return
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
-    losses = eng.last_workspace(B).losses if mode == "clear" else eng.last_workspace(B).losses
-    finite = bool(torch.isfinite(losses[:4]).all())
-    eng.sync_host_state()
 
-    roof = None
-    if not args.no_kernel_pass:
-        G = eng.graphs[B]
-        km = kernel_pass(eng, G)
-        best = None
-        for label, ms in km.items():
-            fl = gemm_flops_of(label, G, eng)
-            if fl is None:
-                continue
-            if best is None or ms > best[1]:
-                best = (label, ms, fl)
-        if best is not None:
-            label, ms, fl = best
-            ach = fl / (ms * 1e-3) / 1e12
-            peak = PEAK_BF16_TFLOPS if hp.get("precision") == "bf16" else PEAK_FP32_TFLOPS
-            roof = {"bound": "mfma", "kernel": label, "achieved": round(ach, 3), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-                    "kernel_ms": round(ms, 5), "flops_per_launch": fl}
-            # HBM bytes per launch of the same call from the committed rocprofv3 PMC passes
-            # (profiles/pmc_traffic.py), when they were taken on this call
-            tpath = os.path.join(ROOT, "profiles", f"{args.config}_traffic.json")
-            if os.path.exists(tpath):
-                try:
-                    t = json.load(open(tpath))["calls"].get(label.split(":")[0])
-                    if t is not None:
-                        roof["traffic"] = round(float(t["traffic_bytes"]))
-                except (OSError, ValueError, KeyError):
-                    pass
-        step_ms_eager = sum(km.values())
-        if args.kernel_table and rank == 0:
-            with open(args.kernel_table, "w") as fh:
-                fh.write(f"{'call':60s} {'ms':>9s} {'GFLOP':>9s} {'TF/s':>8s}\n")
-                for label, ms in sorted(km.items(), key=lambda kv: -kv[1]):
-                    fl = gemm_flops_of(label, G, eng)
-                    fh.write(f"{label:60s} {ms:9.4f} {(fl or 0) / 1e9:9.3f} "
-                             f"{(fl or 0) / (ms * 1e-3) / 1e12:8.2f}\n")
-                fh.write(f"{'total':60s} {step_ms_eager:9.4f}\n")
-    else:
-        step_ms_eager = None
-
+    res = run_workload(args.config, cfg, args.steps, args.warmup, device, world, rank,
+                       detail=not args.no_kernel_pass, kernel_table=args.kernel_table)
+    c3 = None
+    if args.config == "mnist" and world == 1 and not args.no_c3 and args.batch is None:
+        ccfg = CONFIGS["celeba-mim"]
+        k3 = min(args.steps, 60)
+        r3 = run_workload("celeba-mim", ccfg, k3, 5, device, 1, 0, detail=not args.no_kernel_pass)
+        c3 = {"metric": "training images/sec (configs[2])", "value": round(r3["value"], 1), "unit": "images/s",
+              "ms_per_step": round(r3["ms_per_step"], 4), "steps": k3, "warmup": 5, "dtype": "fp32",
+              "config": workload_label("celeba-mim", ccfg, 1),
+              "algorithmic_tflops": round(r3["algorithmic_tflops"], 3), "losses_finite": r3["finite"],
+              "roofline": r3.get("roofline")}
     if rank == 0:
-        value = world * B * args.steps / el
         rec = {
             "metric": "training images/sec at bs=512; ELBO rel-err vs CPU ref",
-            "value": round(value, 1),
+            "value": round(res["value"], 1),
             "unit": "images/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "ms_per_step": round(res["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": hp.get("precision", "fp32"),
             "data": "synthetic U[0,1) images, uniform labels, resident in HBM; deterministic random-init weights",
-            "config": {"workload": f"{args.config}: CLEAR-{'VAE' if mode == 'clear' else 'MIM (CLUB-S)'} {arch} "
-                                   f"z={z} {C}x{hw}x{hw} per-GPU bs={B}", "model": arch, "global_batch": world * B,
-                       "seq_len": None, "parallelism": f"dp{world}"},
-            "algorithmic_tflops": round(conv_flops_per_image(eng.spec) * value / 1e12, 3),
-            "losses_finite": finite,
-            "roofline": roof,
-            "eager_kernel_sum_ms": round(step_ms_eager, 4) if step_ms_eager else None,
+            "config": workload_label(args.config, cfg, world),
+            "algorithmic_tflops": round(res["algorithmic_tflops"], 3),
+            "losses_finite": res["finite"],
+            "roofline": res.get("roofline"),
+            "instep_sum_ms": round(res["instep_sum_ms"], 4) if "instep_sum_ms" in res else None,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if world == 1:
             try:
-                rec["cpu_baseline"] = cpu_baseline(cfg)
-            except Exception as e:  # pragma: no cover
-                rec["cpu_baseline"] = {"error": repr(e)}
-            try:
-                rec["elbo_rel_err"] = elbo_rel_err(cfg, device)
+                rec.update(step_error(cfg, device))
             except Exception as e:  # pragma: no cover
                 rec["elbo_rel_err"] = repr(e)
+            if c3 is not None:
+                try:
+                    c3.update(step_error(CONFIGS["celeba-mim"], device))
+                except Exception as e:  # pragma: no cover
+                    c3["elbo_rel_err"] = repr(e)
+                rec["c3"] = c3
+            if not args.no_cpu_baseline:
+                try:
+                    rec["cpu_baseline"] = cpu_baseline(cfg)
+                except Exception as e:  # pragma: no cover
+                    rec["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

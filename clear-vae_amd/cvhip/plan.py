@@ -15,6 +15,7 @@ program into a HIP graph, the autograd path runs it eagerly.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -378,6 +379,12 @@ def ep_bwd(bnv: BNView, ey: torch.Tensor, relu: bool, stat_div: int = 1) -> cv_e
 
 
 _SIDE_STREAMS: dict = {}
+# Weight-gradient calls on a second stream: off by default.  In a replayed graph every cross-stream edge
+# costs ~10 us of idle time on both queues (rocprofv3 kernel trace of the MNIST step, round 2), and the
+# overlapped GEMMs slow each other down (each grid already fills the chip), so one stream measured as fast
+# or faster on both bench configs (MNIST 0.7015 vs 0.7046 ms, CelebA-MIM 6.46 vs 6.60 ms).
+# CVHIP_SIDE_STREAM=1 restores the two-stream schedule.
+SIDE_STREAM = os.environ.get("CVHIP_SIDE_STREAM", "0") == "1"
 
 
 def _side_stream(device) -> "torch.cuda.Stream":
@@ -419,37 +426,51 @@ class Program:
         self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 0))
 
     def add_side(self, name: str, *args):
-        self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1))
+        self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1 if SIDE_STREAM else 0))
 
     def extend(self, other: "Program"):
         self.calls += other.calls
         self.keep += other.keep
 
-    def run(self, stream: int | None = None, join: bool | None = None):
+    def run(self, stream: int | None = None, join: bool | None = None, timer: list | None = None):
         """join=False leaves the side stream running past the end of the program (a later program's
-        run joins it: the side stream is one ordered queue); graph capture needs a join before its end."""
+        run joins it: the side stream is one ordered queue); graph capture needs a join before its end.
+        timer (eager measurement only, bench.py): a list that receives (call index, start, end) timing
+        events recorded around each call on the stream the call runs on."""
         s = _lib.stream_handle() if stream is None else stream
+        main = torch.cuda.current_stream()
         if not any(c[3] for c in self.calls):
-            for name, fn, args, _ in self.calls:
+            for i, (name, fn, args, _) in enumerate(self.calls):
+                if timer is not None:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(main)
                 rc = fn(*args, s)
                 if rc != 0:
                     _lib.check(rc, name)
+                if timer is not None:
+                    e1.record(main)
+                    timer.append((i, e0, e1))
             return
-        main = torch.cuda.current_stream()
         side = _side_stream(main.device)
         if self._events is None:  # created on the first (eager) run, reused by graph capture
             nf = sum(1 for i, c in enumerate(self.calls) if c[3] and (i == 0 or not self.calls[i - 1][3]))
             self._events = [torch.cuda.Event() for _ in range(nf + 1)]
         ev = 0
         prev_lane = 0
-        for name, fn, args, lane in self.calls:
+        for i, (name, fn, args, lane) in enumerate(self.calls):
             if lane and not prev_lane:  # fork: the side stream waits for the main-stream work so far
                 self._events[ev].record(main)
                 side.wait_event(self._events[ev])
                 ev += 1
+            if timer is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side if lane else main)
             rc = fn(*args, side.cuda_stream if lane else s)
             if rc != 0:
                 _lib.check(rc, name)
+            if timer is not None:
+                e1.record(side if lane else main)
+                timer.append((i, e0, e1))
             prev_lane = lane
         if self.join_at_end if join is None else join:
             self._events[ev].record(side)

@@ -33,6 +33,14 @@ def offset_tensor(device) -> tuple[int, torch.Tensor]:
     return st
 
 
+def reset_counters():
+    """Restart every device's Philox stream at counter 0 (what a fresh process after
+    torch.manual_seed(s) sees).  Engines and the module path share one counter per (device, seed), so
+    consecutive engines draw fresh noise; call this to replay a stream from its start."""
+    for _, off in _state.values():
+        off.zero_()
+
+
 def inject_noise(tensors):
     """Queue eps tensors (one per sample() call, shaped like its mu) for the next draws."""
     _noise_q.extend(tensors)

@@ -266,8 +266,11 @@ def test_graph_replay_matches_eager():
     sd = R.det_state(arch, zt, C)
     hp = {"temperature": 0.1, "alpha": 100.0, "beta": 0.125, "ps": True, "loc": 0, "scale": 1}
     outs = []
+    from cvhip import rng
+
     for graphs in (False, True):
         torch.manual_seed(123)
+        rng.reset_counters()  # the engines share the device Philox stream: replay it from the start
         tr = _fused_trainer(arch, zt, C, sd, hp)
         eng = ClearStep.build(tr, "clear")
         eng.graphs_enabled = graphs
