@@ -368,68 +368,91 @@ __global__ __launch_bounds__(256) void declinear_mask_kernel(int n, int F, int p
   }
 }
 
-template <int KPT>
+// dW[f][k] += sum_n BNbwd(dz)[n][f] * z[n][k].  One workgroup owns DW_F consecutive storage columns and
+// reduces over ALL n rows itself (64-row chunks, the next chunk's loads in flight while the current one
+// is contracted), so every weight-gradient element has one writer: no atomics, deterministic.  (The
+// round-1 version split the rows over 8 workgroups and met in fp32 atomics on addresses `pix` features
+// apart: 31 us at MNIST shape.)  thread t: column t % DW_F, row group / k group t / DW_F.
+constexpr int DW_F = 16;
+constexpr int DW_G = 256 / DW_F;          // 16 row groups (loads) / k groups (contraction)
+
+// RPT rows per thread per chunk (chunk = DW_G * RPT rows): as many as the LDS images allow, so the whole
+// batch arrives in one or two load rounds instead of one exposed latency per 64 rows
+template <int KPT, int RPT>
 __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int K, int pix, int ch,
                                                               const float* __restrict__ dz,
                                                               const float* __restrict__ h, const cv_bn b,
                                                               const float* __restrict__ z, float* gw) {
-  __shared__ float sd[DL_R][DL_F + 1];
-  __shared__ float sz[DL_R][4 * KPT + 1];
-  __shared__ double part[4][4][DL_F];
-  __shared__ BnBwdC kbs[DL_F];
+  constexpr int DW_R = DW_G * RPT;
+  __shared__ float sd[DW_R][DW_F + 1];
+  __shared__ float sz[DW_R][DW_G * KPT + 1];
+  __shared__ BnBwdC kbs[DW_F];
   const int t = threadIdx.x;
-  const int c0 = blockIdx.x * DL_F, r0 = blockIdx.y * DL_R;
-  const int cl = t % DL_F, rg = t / DL_F;
+  const int c0 = blockIdx.x * DW_F;
+  const int cl = t % DW_F, rg = t / DW_F;
   const int col = c0 + cl;
-  const int f = col < F ? dl_feature(col, pix, ch) : 0;
-  float dv[DL_RPT], hv[DL_RPT];
+  const bool live = col < F;
+  const int f = live ? dl_feature(col, pix, ch) : 0;
+  constexpr int KW = DW_G * KPT;           // z columns staged per chunk (>= K)
+  constexpr int ZPT = (DW_R * KW + 255) / 256;
+  float dv[RPT], hv[RPT], zv[ZPT];
+  auto fetch = [&](int r0) {
 #pragma unroll
-  for (int i = 0; i < DL_RPT; ++i) {
-    const int r = r0 + rg + 4 * i;
-    dv[i] = 0.f;
-    hv[i] = 0.f;
-    if (col < F && r < n) {
-      dv[i] = dz[(size_t)r * F + col];
-      hv[i] = h[(size_t)r * F + col];
+    for (int i = 0; i < RPT; ++i) {
+      const int r = r0 + rg + DW_G * i;
+      const bool ok = live && r < n;
+      dv[i] = ok ? dz[(size_t)r * F + col] : 0.f;
+      hv[i] = ok ? h[(size_t)r * F + col] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < ZPT; ++j) {
+      const int e = t + 256 * j;
+      const int rr = e / KW, kk = e - rr * KW;
+      zv[j] = (e < DW_R * KW && r0 + rr < n && kk < K) ? z[(size_t)(r0 + rr) * K + kk] : 0.f;
+    }
+  };
+  fetch(0);
+  // BN1d backward constants of the block's columns (replica fold, one thread per column)
+  if (t < DW_F) {
+    double s = 0.0, q = 0.0, gs = 0.0, gq = 0.0;
+    if (live) {
+      bn_sums(b.stat, F, f, s, q);
+      bn_sums(b.gstat, F, f, gs, gq);
+      kbs[t] = bn_bwd_const_s(b, f, s, q, gs, gq);
     }
   }
-  constexpr int ZPT = (DL_R * 4 * KPT + 255) / 256;
-  float zv[ZPT];
-#pragma unroll
-  for (int j = 0; j < ZPT; ++j) {
-    const int e = t + 256 * j;
-    const int rr = e / (4 * KPT), kk = e % (4 * KPT);
-    zv[j] = (e < DL_R * 4 * KPT && r0 + rr < n && kk < K) ? z[(size_t)(r0 + rr) * K + kk] : 0.f;
-  }
-  dl_fold(b, true, f, col < F, part, nullptr, kbs);
-  BnBwdC kb;
-  if (col < F) kb = kbs[cl];
-#pragma unroll
-  for (int i = 0; i < DL_RPT; ++i) {
-    const int r = r0 + rg + 4 * i;
-    sd[rg + 4 * i][cl] = (col < F && r < n) ? bn_bwd(dv[i], hv[i], kb) : 0.f;
-  }
-#pragma unroll
-  for (int j = 0; j < ZPT; ++j) {
-    const int e = t + 256 * j;
-    if (e < DL_R * 4 * KPT) sz[e / (4 * KPT)][e % (4 * KPT)] = zv[j];
-  }
   __syncthreads();
-  const int kg = rg;
+  BnBwdC kb;
+  if (live) kb = kbs[cl];
   float acc[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) acc[j] = 0.f;
-  const int rmax = min(DL_R, n - r0);
-  for (int rr = 0; rr < rmax; ++rr) {
-    const float d = sd[rr][cl];
+  for (int r0 = 0; r0 < n; r0 += DW_R) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) acc[j] = fmaf(d, sz[rr][kg + 4 * j], acc[j]);
+    for (int i = 0; i < RPT; ++i) {
+      const int r = r0 + rg + DW_G * i;
+      sd[rg + DW_G * i][cl] = (live && r < n) ? bn_bwd(dv[i], hv[i], kb) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < ZPT; ++j) {
+      const int e = t + 256 * j;
+      if (e < DW_R * KW) sz[e / KW][e % KW] = zv[j];
+    }
+    __syncthreads();
+    if (r0 + DW_R < n) fetch(r0 + DW_R);
+    const int rmax = min(DW_R, n - r0);
+    for (int rr = 0; rr < rmax; ++rr) {
+      const float d = sd[rr][cl];
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) acc[j] = fmaf(d, sz[rr][rg * KPT + j], acc[j]);
+    }
+    __syncthreads();
   }
-  if (col < F) {
+  if (live) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
-      const int kk = kg + 4 * j;
-      if (kk < K) atomicAdd(gw + (size_t)f * K + kk, acc[j]);
+      const int kk = rg * KPT + j;
+      if (kk < K) gw[(size_t)f * K + kk] += acc[j];
     }
   }
 }
@@ -636,18 +659,16 @@ extern "C" int cv_declinear_backward_weight(const cv_linear* g, float* da, const
   cv_bn b2 = *bn;
   if (gstat_out) b2.gstat = gstat_out;  // (else: da already masked, bn->gstat complete)
   CV_REQUIRE(b2.gstat != nullptr, "declinear_backward_weight: BN1d backward sums missing");
-  if (K <= 16)
-    hipLaunchKernelGGL(declinear_wgrad_kernel<4>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
-                       b2, zin, gweight);
-  else if (K <= 32)
-    hipLaunchKernelGGL(declinear_wgrad_kernel<8>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
-                       b2, zin, gweight);
-  else if (K <= 64)
-    hipLaunchKernelGGL(declinear_wgrad_kernel<16>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
-                       b2, zin, gweight);
-  else
-    hipLaunchKernelGGL(declinear_wgrad_kernel<32>, grid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, da, h,
-                       b2, zin, gweight);
+  const dim3 wgrid(cdiv(F, DW_F));
+#define CV_DW(KPT_, RPT_)                                                                                     \
+  hipLaunchKernelGGL((declinear_wgrad_kernel<KPT_, RPT_>), wgrid, dim3(256), 0, S(stream), g->n, F, K, pix, g->out_ch, \
+                     da, h, b2, zin, gweight)
+  // (static LDS <= 40 KB: chunk rows x (DW_F + 16 KPT + 2) floats)
+  if (K <= DW_G) CV_DW(1, 16);
+  else if (K <= 2 * DW_G) CV_DW(2, 12);
+  else if (K <= 4 * DW_G) CV_DW(4, 8);
+  else CV_DW(8, 4);
+#undef CV_DW
   CV_LAUNCH_CHECK("declinear_wgrad");
   return 0;
 }

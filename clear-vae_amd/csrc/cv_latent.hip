@@ -118,19 +118,33 @@ __global__ __launch_bounds__(1024) void kl_kernel(const float* __restrict__ mu, 
 
 // Fused step version: dheads = [dmu_c, dlv_c, dmu_s, dlv_s] from KL (weight w from the annealer) and
 // the decoder gradient dz through z = mu + eps*exp(lv/2).  losses[1..2] = kl_c, kl_s; losses[7] = w.
-__global__ __launch_bounds__(1024) void combine_kernel(const float* __restrict__ heads, const float* __restrict__ z,
-                                                       const float* __restrict__ dz, int n, int d, float beta,
-                                                       float loc, float scale, const int64_t* anneal_step,
-                                                       const double* rec_in, float* __restrict__ dheads,
-                                                       float* losses) {
-  __shared__ double scratch[16];
-  const double t = (double)anneal_step[0];
+struct CombineArgs {
+  const float* heads;
+  const float* z;
+  const float* dz;
+  int n, d;
+  float beta, loc, scale;
+  const int64_t* anneal_step;
+  const double* rec_in;
+  float* dheads;
+  float* losses;
+};
+
+template <int NTH>
+__device__ __forceinline__ void combine_body(const CombineArgs& C, double* scratch) {
+  const float* __restrict__ heads = C.heads;
+  const float* __restrict__ z = C.z;
+  const float* __restrict__ dz = C.dz;
+  float* __restrict__ dheads = C.dheads;
+  const int n = C.n, d = C.d;
+  const double t = (double)C.anneal_step[0];
+  const float beta = C.beta, loc = C.loc, scale = C.scale;
   // LogisticAnnealer.slope (trainer.py:32-34): beta / (1 + exp(-(t - loc)/scale)), in double
   const float w = (float)((double)beta / (1.0 + exp(-(t - (double)loc) / (double)scale)));
   const float inv_n = 1.0f / (float)n;
   double sc = 0.0, ss = 0.0;
   const int zd = 2 * d;
-  for (int e = threadIdx.x; e < n * zd; e += blockDim.x) {
+  for (int e = threadIdx.x; e < n * zd; e += NTH) {
     const int r = e / zd, j = e % zd;
     const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
     const float m = heads[(size_t)r * 4 * d + blk * d + k];
@@ -143,18 +157,23 @@ __global__ __launch_bounds__(1024) void combine_kernel(const float* __restrict__
     dheads[(size_t)r * 4 * d + blk * d + k] = w * m * inv_n + g;
     dheads[(size_t)r * 4 * d + (blk + 1) * d + k] = w * (-0.5f * inv_n) * (1.0f - el) + g * (zz - m) * 0.5f;
   }
-  const double kc = block_sum<1024>(sc, scratch);
-  const double ks = block_sum<1024>(ss, scratch);
+  const double kc = block_sum<NTH>(sc, scratch);
+  const double ks = block_sum<NTH>(ss, scratch);
   if (threadIdx.x == 0) {
-    if (rec_in) {
+    if (C.rec_in) {
       double r = 0.0;
-      for (int q = 0; q < CV_REC_REPL; ++q) r += rec_in[q];
-      losses[0] = (float)r;
+      for (int q = 0; q < CV_REC_REPL; ++q) r += C.rec_in[q];
+      C.losses[0] = (float)r;
     }
-    losses[1] = (float)(-0.5 * kc / (double)n);
-    losses[2] = (float)(-0.5 * ks / (double)n);
-    losses[7] = w;
+    C.losses[1] = (float)(-0.5 * kc / (double)n);
+    C.losses[2] = (float)(-0.5 * ks / (double)n);
+    C.losses[7] = w;
   }
+}
+
+__global__ __launch_bounds__(1024) void combine_kernel(const CombineArgs C) {
+  __shared__ double scratch[16];
+  combine_body<1024>(C, scratch);
 }
 
 // ---------------------------------------------------------------- reconstruction MSE (autograd path)
@@ -201,6 +220,10 @@ struct NtArgs {
   int n, d, sim;
   float tau;
   int accumulate;
+  int nbr;
+  int rpb;            // rows per 256-thread block of the LDS kernels (a multiple of 4: one row per wave per pass)
+  int with_combine;   // rows kernel: the block with blockIdx.y == nbr runs the latent combine (cmb)
+  CombineArgs cmb;
 };
 
 constexpr int NT_ROWS = 4;   // rows (waves) per 256-thread block
@@ -606,6 +629,10 @@ __device__ __forceinline__ void ntl_theta(const NtLds& L, int r, int d, float* m
 template <int DM>
 __global__ __launch_bounds__(256) void ntxent_rows_lds_kernel(const NtArgs A) {
   extern __shared__ __attribute__((aligned(16))) char ntl_smem[];
+  if (blockIdx.y >= (unsigned)A.nbr) {  // the fused latent step's combine block (independent of the rows)
+    if (A.with_combine && blockIdx.x == 0) combine_body<256>(A.cmb, reinterpret_cast<double*>(ntl_smem));
+    return;
+  }
   const Branch& b = A.br[blockIdx.y];
   const int n = A.n, d = A.d;
   const bool cosine = A.sim == CV_SIM_COSINE;
@@ -613,8 +640,8 @@ __global__ __launch_bounds__(256) void ntxent_rows_lds_kernel(const NtArgs A) {
   NtLds L = ntl_carve(ntl_smem, n, d, need_lv, false);
   ntl_stage(b, A.label, n, d, need_lv, cosine, false, L);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int iend = min(n, (int)(blockIdx.x + 1) * NTL_ROWS);
-  for (int i = blockIdx.x * NTL_ROWS + w; i < iend; i += 4) {
+  const int iend = min(n, (int)(blockIdx.x + 1) * A.rpb);
+  for (int i = blockIdx.x * A.rpb + w; i < iend; i += 4) {
     float mi[DM], li[DM], mj[DM], lj[DM];
     ntl_theta<DM>(L, i, d, mi, li, need_lv);
     const long long lab = L.lab[i];
@@ -672,8 +699,8 @@ __global__ __launch_bounds__(256) void ntxent_grad_lds_kernel(const NtArgs A) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float gup = b.gmul * (b.gscale ? b.gscale[0] : 1.0f);
   const float c = (nf > 0.f) ? gup / (nf * A.tau) : 0.f;
-  const int iend = min(n, (int)(blockIdx.x + 1) * NTL_ROWS);
-  for (int i = blockIdx.x * NTL_ROWS + w; i < iend; i += 4) {
+  const int iend = min(n, (int)(blockIdx.x + 1) * A.rpb);
+  for (int i = blockIdx.x * A.rpb + w; i < iend; i += 4) {
     float mi[DM], li[DM], mj[DM], lj[DM], gm[DM], gl[DM];
     ntl_theta<DM>(L, i, d, mi, li, need_lv);
 #pragma unroll
@@ -734,9 +761,15 @@ struct DDispatch;
 // LDS-staged variants when the branch fits (the common case); the global-walk kernels otherwise
 static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st) {
   const bool need_lv = !(a.sim == CV_SIM_COSINE || a.sim == CV_SIM_L2);
-  const size_t lds = ntl_bytes(a.n, a.d, need_lv, !rows);
+  size_t lds = ntl_bytes(a.n, a.d, need_lv, !rows);
   if (lds > 144 * 1024) return -1;
-  const dim3 grid(cdiv(a.n, NTL_ROWS), nbr);
+  if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);  // (the combine block's reduction scratch)
+  // one row per wave: the pair loops, not the per-block staging of the branch, dominate (16-row blocks,
+  // i.e. a quarter of the blocks, measured 2x slower at MNIST bs=512)
+  NtArgs arg = a;
+  arg.rpb = NTL_ROWS;
+  arg.nbr = nbr;
+  const dim3 grid(cdiv(a.n, arg.rpb), nbr + ((rows && a.with_combine) ? 1 : 0));
   const void* kern;
   if (a.d <= 8) kern = rows ? (const void*)ntxent_rows_lds_kernel<8> : (const void*)ntxent_grad_lds_kernel<8>;
   else if (a.d <= 16) kern = rows ? (const void*)ntxent_rows_lds_kernel<16> : (const void*)ntxent_grad_lds_kernel<16>;
@@ -746,7 +779,6 @@ static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st
     (void)hipGetLastError();
     return -1;
   }
-  NtArgs arg = a;
   void* params[] = {&arg};
   if (hipLaunchKernel(kern, grid, dim3(256), params, lds, st) != hipSuccess) {
     ::cv::set_error("%s: launch failed", rows ? "ntxent_rows" : "ntxent_grad");
@@ -758,6 +790,10 @@ static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st
 static int ntxent_launch(const NtArgs& a, int nbr, bool rows, hipStream_t st) {
   const int r = ntxent_launch_lds(a, nbr, rows, st);
   if (r >= 0) return r;
+  if (rows && a.with_combine) {  // the global-walk kernels have no combine block
+    hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, st, a.cmb);
+    CV_LAUNCH_CHECK("latent_combine");
+  }
   dim3 grid(cdiv(a.n, NT_ROWS), nbr);
   if (a.d <= 8) {
     if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<8>, grid, dim3(256), 0, st, a);
@@ -839,8 +875,8 @@ extern "C" int cv_latent_combine(const float* heads, const float* z, const float
                                  float* dheads, float* losses, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine: bad args");
-  hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), heads, z, dz, n, d, beta, loc, scale,
-                     anneal_step, rec_in, dheads, losses);
+  const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses};
+  hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), C);
   CV_LAUNCH_CHECK("latent_combine");
   return 0;
 }
@@ -866,13 +902,11 @@ extern "C" int cv_mse_sum(const float* xhat, const float* x, int n, int per_samp
   return 0;
 }
 
-extern "C" int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
-                         float temperature, int phase, int accumulate, cv_stream_t stream) {
-  clear_error();
+static int ntxent_args(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
+                       float temperature, int accumulate, NtArgs& a) {
   CV_REQUIRE(br && nbr >= 1 && nbr <= MAXBR && label && n > 0 && d > 0 && d <= 64, "ntxent: bad args (d<=64)");
   CV_REQUIRE(n <= NT_MAXN, "ntxent: batch %d > %d", n, NT_MAXN);
   CV_REQUIRE(sim >= CV_SIM_COSINE && sim <= CV_SIM_MAHALANOBIS, "unimplemented similarity measure.");
-  NtArgs a;
   memset(&a, 0, sizeof(a));
   for (int i = 0; i < nbr; ++i) {
     CV_REQUIRE(br[i].mu && br[i].lse, "ntxent: branch %d incomplete", i);
@@ -896,11 +930,39 @@ extern "C" int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* lab
   a.sim = sim;
   a.tau = temperature;
   a.accumulate = accumulate;
+  return 0;
+}
+
+extern "C" int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
+                         float temperature, int phase, int accumulate, cv_stream_t stream) {
+  clear_error();
+  NtArgs a;
+  if (ntxent_args(br, nbr, label, n, d, sim, temperature, accumulate, a)) return 1;
   if (phase == 0 || phase == 2) {
     if (ntxent_launch(a, nbr, true, S(stream))) return 2;
   }
   if (phase == 1 || phase == 2) {
     if (ntxent_launch(a, nbr, false, S(stream))) return 2;
   }
+  return 0;
+}
+
+extern "C" int cv_latent_step(const float* heads, const float* z, const float* dz, int n, int d, float beta,
+                              float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                              float* dheads, float* losses, const cv_ntxent_branch* br, int nbr,
+                              const int64_t* label, int sim, float temperature, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_step: bad args");
+  NtArgs a;
+  if (ntxent_args(br, nbr, label, n, d, sim, temperature, 1, a)) return 1;
+  for (int i = 0; i < nbr; ++i)
+    CV_REQUIRE(br[i].dmu == nullptr || (br[i].dmu >= dheads && br[i].dmu < dheads + (size_t)n * 4 * d),
+               "latent_step: branch %d gradient must land in dheads", i);
+  a.with_combine = 1;
+  a.cmb = CombineArgs{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses};
+  // launch 1: row log-sum-exps of every branch + the KL / decoder-chain seed of dheads (independent);
+  // launch 2: contrastive losses and their gradients accumulated into dheads
+  if (ntxent_launch(a, nbr, true, S(stream))) return 2;
+  if (ntxent_launch(a, nbr, false, S(stream))) return 2;
   return 0;
 }

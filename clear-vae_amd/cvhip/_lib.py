@@ -196,6 +196,11 @@ _SIGS = {
         c_int,
         [_P(cv_ntxent_branch), c_int, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
     ),
+    "cv_latent_step": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
+         c_void_p, _P(cv_ntxent_branch), c_int, c_void_p, c_int, c_float, c_void_p],
+    ),
     "cv_mi_workspace_bytes": (c_size_t, [c_int]),
     "cv_mi_forward": (
         c_int,

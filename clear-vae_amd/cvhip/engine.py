@@ -266,9 +266,6 @@ class ClearStep:
 
         # latent terms -> d(heads)
         lat = Program()
-        lat.add("cv_latent_combine", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
-                ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
-                ws.rec, ws.dheads, ws.losses)
         hb = ws.heads.data_ptr()
         dh = ws.dheads.data_ptr()
         alpha = float(hp["alpha"])
@@ -281,7 +278,11 @@ class ClearStep:
                                              None, alpha if ps else -alpha, ws.losses.data_ptr() + 16,
                                              ws.lse[1].data_ptr()))
         arr = (cv_ntxent_branch * len(branches))(*branches)
-        lat.add("cv_ntxent", arr, len(branches), lab, n, d, self.sim, ctypes.c_float(tau), 2, 1)
+        # KL + decoder chain into d(heads), then the contrastive terms accumulated on top: two launches
+        lat.add("cv_latent_step", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
+                ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
+                ws.rec, ws.dheads, ws.losses, arr, len(branches), lab, self.sim, ctypes.c_float(tau))
+        lat.keep.append(arr)
         lat_inj = Program()
         lat_inj.extend(lat)
         if self.mode == "mim":

@@ -262,6 +262,15 @@ typedef struct cv_ntxent_branch {
 int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
               float temperature, int phase, int accumulate, cv_stream_t stream);
 
+/* The fused step's latent terms in two launches (trainer.py:452-480): cv_latent_combine (KL with the
+ * annealer weight, the decoder gradient chained through z) and cv_ntxent phase 2 with accumulate = 1
+ * on the same dheads.  The combine runs as an extra workgroup of the row-log-sum-exp launch (it does
+ * not depend on it); every branch's dmu / dlogvar must point into dheads. */
+int cv_latent_step(const float* heads, const float* z, const float* dz, int n, int d, float beta,
+                   float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                   float* dheads, float* losses, const cv_ntxent_branch* br, int nbr,
+                   const int64_t* label, int sim, float temperature, cv_stream_t stream);
+
 /* ---- MI upper bounds (mi_estimator.py:108-198) ---- */
 enum { CV_MI_NONE = 0, CV_MI_CLUBSAMPLE = 1, CV_MI_L1OUT = 2 };
 
