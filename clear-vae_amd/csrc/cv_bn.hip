@@ -457,6 +457,92 @@ __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int 
   }
 }
 
+// ---------------------------------------------------------------- end-of-backward reduction (cv_step_reduce)
+// One launch for everything between the last backward GEMM and the optimizer: the split-K partial tiles of
+// every deferred weight gradient (summed in fixed split order: one writer per element, deterministic), the
+// BatchNorm affine gradients from the backward sums, and the running statistics from the forward sums.
+// Replaces one wgrad_reduce launch per weight gradient, cv_bn_param_grads (x2) and cv_bn_update_running.
+constexpr int MAX_DEFER = 24;
+struct StepRedArgs {
+  cv_wgrad_defer d[MAX_DEFER];
+  int blk0[MAX_DEFER + 1];  // prefix sums of the reduction blocks of each deferred gradient
+  int nd;
+  cv_bn bn[MAX_BN];
+  float* dg[MAX_BN];
+  float* db[MAX_BN];
+  int64_t* nbt[MAX_BN];
+  int nbn, grads, running;
+  float momentum;
+};
+constexpr int SR_E = 64;  // partial-tile elements per block (4 waves split the split range)
+
+__global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
+  __shared__ float red[4][SR_E];
+  __shared__ double scratch[4 * 256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (b < a.blk0[a.nd]) {
+    int di = 0;
+    while (di + 1 < a.nd && b >= a.blk0[di + 1]) ++di;
+    const cv_wgrad_defer& d = a.d[di];
+    const int ol = t & 63, zg = t >> 6;
+    const long o = (long)(b - a.blk0[di]) * SR_E + ol;
+    const long total = (long)d.M * d.ntot;
+    const size_t sstride = (size_t)total;
+    float acc = 0.f;
+    if (o < total) {
+      const float* p = d.part + o;
+      int z = zg;
+      for (; z + 12 < d.split; z += 16) {
+        const float a0 = p[(size_t)z * sstride], a1 = p[(size_t)(z + 4) * sstride];
+        const float a2 = p[(size_t)(z + 8) * sstride], a3 = p[(size_t)(z + 12) * sstride];
+        acc += (a0 + a1) + (a2 + a3);
+      }
+      for (; z < d.split; z += 4) acc += p[(size_t)z * sstride];
+    }
+    red[zg][ol] = acc;
+    __syncthreads();
+    if (t < SR_E && o < total) {
+      const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+      const int row = (int)(o / d.ntot), col = (int)(o - (long)row * d.ntot);
+      if (col < d.N) {
+        const int tap = col / d.cb, c = col - tap * d.cb;
+        d.gweight[((size_t)row * d.cb + c) * d.kk + tap] += v;
+      } else if (d.gbias) {
+        d.gbias[row] += v;
+      }
+    }
+    return;
+  }
+  const int l = b - a.blk0[a.nd];
+  if (l >= a.nbn) return;
+  const cv_bn& bn = a.bn[l];
+  if (a.grads) {  // dgamma = sum dz*xhat, dbeta = sum dz (the backward sums)
+    cv_bn gb = bn;
+    gb.stat = bn.gstat;
+    float* dg = a.dg[l];
+    float* db = a.db[l];
+    bn_fold<256>(gb, false, scratch, [&](int c, double s1, double s2, double, double) {
+      if (db) db[c] = (float)s1;
+      if (dg) dg[c] = (float)s2;
+    });
+  }
+  if (a.running) {  // running statistics, momentum update with the unbiased batch variance
+    if (t == 0 && a.nbt[l]) a.nbt[l][0] += 1;
+    float* rm = const_cast<float*>(bn.running_mean);
+    float* rv = const_cast<float*>(bn.running_var);
+    const float m = a.momentum;
+    bn_fold<256>(bn, false, scratch, [&](int c, double s1, double q, double, double) {
+      const double n = (double)bn.count;
+      const double mean = s1 / n;
+      double var = q / n - mean * mean;
+      if (var < 0.0) var = 0.0;
+      const double unbiased = (bn.count > 1) ? var * n / (n - 1.0) : var;
+      rm[c] = m * (float)mean + (1.0f - m) * rm[c];
+      rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
+    });
+  }
+}
+
 // ---------------------------------------------------------------- multi-buffer zero
 struct ZeroArgs {
   uint32_t* p[8];
@@ -670,5 +756,48 @@ extern "C" int cv_declinear_backward_weight(const cv_linear* g, float* da, const
   else CV_DW(8, 4);
 #undef CV_DW
   CV_LAUNCH_CHECK("declinear_wgrad");
+  return 0;
+}
+
+extern "C" int cv_step_reduce(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn, float* const* dgamma,
+                              float* const* dbeta, int running, float momentum, int64_t* const* nbt,
+                              cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(ndefer >= 0 && ndefer <= MAX_DEFER && nbn >= 0 && nbn <= MAX_BN, "step_reduce: <= %d gradients, <= %d BN layers",
+             MAX_DEFER, MAX_BN);
+  CV_REQUIRE(ndefer == 0 || defers, "step_reduce: null defer list");
+  CV_REQUIRE(nbn == 0 || bn, "step_reduce: null BN list");
+  StepRedArgs a;
+  memset(&a, 0, sizeof(a));
+  int nb = 0;
+  for (int i = 0; i < ndefer; ++i) {
+    const cv_wgrad_defer& d = defers[i];
+    a.blk0[a.nd] = nb;
+    if (d.split <= 0) continue;  // that weight gradient was written directly
+    CV_REQUIRE(d.part && d.gweight && d.M > 0 && d.ntot > 0 && d.N <= d.ntot && d.cb > 0 && d.kk > 0,
+               "step_reduce: deferred gradient %d incomplete", i);
+    a.d[a.nd] = d;
+    nb += cdiv((long)d.M * d.ntot, SR_E);
+    ++a.nd;
+  }
+  a.blk0[a.nd] = nb;
+  for (int i = 0; i < nbn; ++i) {
+    CV_REQUIRE(bn[i].C > 0 && bn[i].count > 0, "step_reduce: BN layer %d incomplete", i);
+    CV_REQUIRE(!dgamma || bn[i].gstat, "step_reduce: BN layer %d has no backward sums", i);
+    CV_REQUIRE(!running || (bn[i].stat && bn[i].running_mean && bn[i].running_var),
+               "step_reduce: BN layer %d has no forward sums / running buffers", i);
+    a.bn[i] = bn[i];
+    a.dg[i] = dgamma ? dgamma[i] : nullptr;
+    a.db[i] = dbeta ? dbeta[i] : nullptr;
+    a.nbt[i] = nbt ? nbt[i] : nullptr;
+  }
+  a.nbn = nbn;
+  a.grads = (dgamma || dbeta) ? 1 : 0;
+  a.running = running;
+  a.momentum = momentum;
+  const int blocks = nb + nbn;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(step_reduce_kernel, dim3(blocks), dim3(256), 0, S(stream), a);
+  CV_LAUNCH_CHECK("step_reduce");
   return 0;
 }

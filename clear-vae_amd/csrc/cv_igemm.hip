@@ -1069,8 +1069,26 @@ static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
   return w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
 }
 
+// Deferred weight gradients (cv_*_backward_weight_deferred): while a sink is set, the split-K partial
+// tiles are left in the caller's workspace and their layout is recorded instead of launching the reduction;
+// cv_step_reduce later sums every deferred gradient of the step in one launch.
+static thread_local cv_wgrad_defer* g_defer_sink = nullptr;
+
 static int launch_wgrad_reduce(const float* part, int split, int M, int N, int ntot, int cb, int kk, float* gw,
                                float* gbias, hipStream_t st) {
+  if (g_defer_sink) {
+    cv_wgrad_defer& d = *g_defer_sink;
+    d.part = part;
+    d.split = split;
+    d.M = M;
+    d.N = N;
+    d.ntot = ntot;
+    d.cb = cb;
+    d.kk = kk;
+    d.gweight = gw;
+    d.gbias = gbias;
+    return 0;
+  }
   const int gx = cdiv((long)M * ntot, 64);
   int gy = cdiv(split, 32);  // <= 32 slabs per block (8 per thread)
   const int zper = cdiv(split, gy);
@@ -1230,6 +1248,18 @@ extern "C" int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, c
   return run_wgrad(geo, in, gout, gweight, nullptr, split_k, work, work_bytes, S(stream), g->mma);
 }
 
+extern "C" int cv_conv_backward_weight_deferred(const cv_conv* g, const cv_operand* in, const cv_operand* gout,
+                                                float* gweight, float* gbias, float* work, size_t work_bytes,
+                                                cv_wgrad_defer* defer, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(defer && work, "conv_backward_weight_deferred: needs a defer record and a workspace");
+  memset(defer, 0, sizeof(*defer));  // split 0: the launch wrote gweight / gbias directly
+  g_defer_sink = defer;
+  const int r = cv_conv_backward_weight(g, in, gout, gweight, gbias, 0, work, work_bytes, stream);
+  g_defer_sink = nullptr;
+  return r;
+}
+
 // ---------------------------------------------------------------- linear layers
 static int linear_launch(Args& a, int accumulate, hipStream_t st) {
   int BM_, BN_;
@@ -1346,4 +1376,16 @@ extern "C" int cv_linear_backward_weight(const cv_linear* g, const cv_operand* g
   geo.s = 1;
   geo.p = 0;
   return run_wgrad(geo, gout, in, gweight, gbias, split_k, work, work_bytes, S(stream), g->mma);
+}
+
+extern "C" int cv_linear_backward_weight_deferred(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
+                                                  float* gweight, float* gbias, float* work, size_t work_bytes,
+                                                  cv_wgrad_defer* defer, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(defer && work, "linear_backward_weight_deferred: needs a defer record and a workspace");
+  memset(defer, 0, sizeof(*defer));
+  g_defer_sink = defer;
+  const int r = cv_linear_backward_weight(g, gout, in, gweight, gbias, 0, work, work_bytes, stream);
+  g_defer_sink = nullptr;
+  return r;
 }

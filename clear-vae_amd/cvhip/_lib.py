@@ -100,6 +100,11 @@ class cv_linear(ctypes.Structure):
     ]
 
 
+class cv_wgrad_defer(ctypes.Structure):
+    _fields_ = [("part", c_void_p), ("split", c_int), ("M", c_int), ("N", c_int), ("ntot", c_int), ("cb", c_int),
+                ("kk", c_int), ("gweight", c_void_p), ("gbias", c_void_p)]
+
+
 class cv_ntxent_branch(ctypes.Structure):
     _fields_ = [
         ("mu", c_void_p),
@@ -142,6 +147,21 @@ _SIGS = {
     "cv_conv_backward_weight": (
         c_int,
         [_P(cv_conv), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p],
+    ),
+    "cv_conv_backward_weight_deferred": (
+        c_int,
+        [_P(cv_conv), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer),
+         c_void_p],
+    ),
+    "cv_linear_backward_weight_deferred": (
+        c_int,
+        [_P(cv_linear), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer),
+         c_void_p],
+    ),
+    "cv_step_reduce": (
+        c_int,
+        [_P(cv_wgrad_defer), c_int, _P(cv_bn), c_int, _P(c_void_p), _P(c_void_p), c_int, c_float, _P(c_void_p),
+         c_void_p],
     ),
     "cv_conv_wgrad_workspace_bytes": (c_size_t, [_P(cv_conv), c_int]),
     "cv_linear_wgrad_workspace_bytes": (c_size_t, [_P(cv_linear), c_int]),

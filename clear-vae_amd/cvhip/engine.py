@@ -40,7 +40,7 @@ from . import _lib, rng
 from . import dist as cvdist
 from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
 from .autograd import est_params, mlp_struct
-from .plan import ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
+from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
 
 
 def _dist_world():
@@ -255,14 +255,20 @@ class ClearStep:
             ws.encoder_program(f, X, True, zero_heads=False)
             ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
             ws.decoder_program(f, ws.z, True, "loss", X)
-            ws.running_program(f, "all")
+            # (the running statistics are folded at the end of the backward by cv_step_reduce)
             return f
 
         fwd, fwd_inj = make_fwd(False), make_fwd(True)
-        # decoder backward (bucket 1 of the gradient arena)
+        # decoder backward (bucket 1 of the gradient arena).  Weight gradients are deferred: their split-K
+        # partial tiles, the BN affine gradients and the running statistics are reduced by one
+        # cv_step_reduce launch at the end of the backward (data parallel: one per gradient bucket, before
+        # the bucket's all-reduce)
+        dp = self.world > 1
+        dec_defer, enc_defer = DeferGroup(), DeferGroup()
         dec = Program()
-        ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False)
-        ws.bn_grads_program(dec, pg, "dec")
+        ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer)
+        if dp:
+            ws.step_reduce_program(dec, dec_defer, pg, "dec", running=False)
 
         # latent terms -> d(heads)
         lat = Program()
@@ -294,8 +300,12 @@ class ClearStep:
                 prog.add("cv_mi_backward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work, None,
                          ctypes.c_float(float(hp["lambda"])), None, None, 0, 1, None, ws.heads, ws.z, ws.dheads, d)
         enc = Program()
-        ws.encoder_backward_program(enc, pg, ws.dheads, x=X)
-        ws.bn_grads_program(enc, pg, "enc")
+        ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer)
+        if dp:  # encoder bucket: its gradients and BN affine grads; every layer's running statistics
+            ws.step_reduce_program(enc, enc_defer, pg, "enc", running=False)
+            ws.running_program(enc, "all")
+        else:
+            ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
         upd = Program()
         upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper, self.adam.step,
                 self.gscale if self.world > 1 else None, self.anneal)

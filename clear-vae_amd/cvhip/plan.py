@@ -35,6 +35,7 @@ from ._lib import (
     cv_epilogue,
     cv_linear,
     cv_operand,
+    cv_wgrad_defer,
 )
 
 # ----------------------------------------------------------------------------- topology
@@ -477,6 +478,25 @@ class Program:
             main.wait_event(self._events[ev])
 
 
+class DeferGroup:
+    """Records of the deferred weight-gradient calls that one cv_step_reduce sums (include/clearvae.h,
+    cv_wgrad_defer): a contiguous array the calls fill at enqueue time."""
+
+    CAP = 24  # MAX_DEFER of cv_step_reduce
+
+    def __init__(self):
+        self.arr = (cv_wgrad_defer * self.CAP)()
+        self.n = 0
+
+    def next(self):
+        if self.n >= self.CAP:
+            raise RuntimeError("more than 24 deferred weight gradients in one cv_step_reduce")
+        ref = ctypes.cast(ctypes.addressof(self.arr) + self.n * ctypes.sizeof(cv_wgrad_defer),
+                          ctypes.POINTER(cv_wgrad_defer))
+        self.n += 1
+        return ref
+
+
 def struct_array(ctype, items):
     arr = (ctype * len(items))(*items)
     return arr
@@ -560,6 +580,38 @@ class Workspace:
                 ctypes.byref(cv_linear(n, spec.F, 4 * d, Hh * Wh, C, 1, 0)), 0)))
             self.wg_bytes = max(wb + [16])
             self.wg_work = torch.empty(self.wg_bytes // 4, **f32)
+            self._defer_work = {}  # deferred weight gradients: one partial-tile region per call
+
+    def _wgrad_call(self, P: "Program", kind: str, geom, a, b, gw, gb, key, defer):
+        """One weight-gradient call.  defer=None: reduced in place (shared split-K workspace).  defer=a
+        DeferGroup: cv_*_backward_weight_deferred with its own workspace, its cv_wgrad_defer record in the
+        group for the step's cv_step_reduce."""
+        L = _lib.lib()
+        if defer is None:
+            if kind == "conv":
+                P.add_side("cv_conv_backward_weight", geom, a, b, gw, gb, 0, self.wg_work, self.wg_bytes)
+            else:
+                P.add_side("cv_linear_backward_weight", geom, a, b, gw, gb, 0, self.wg_work, self.wg_bytes)
+            return
+        nb = int((L.cv_conv_wgrad_workspace_bytes if kind == "conv" else L.cv_linear_wgrad_workspace_bytes)(
+            ctypes.byref(geom), 0))
+        buf = self._defer_work.get(key)
+        if buf is None or buf.numel() * 4 < nb:
+            buf = self._defer_work[key] = torch.empty(max(nb, 16) // 4 + 4, dtype=torch.float32, device=self.device)
+        name = "cv_conv_backward_weight_deferred" if kind == "conv" else "cv_linear_backward_weight_deferred"
+        P.add(name, geom, a, b, gw, gb, buf, buf.numel() * 4, defer.next())
+
+    def step_reduce_program(self, P: "Program", defer: "DeferGroup", param_grad, which: str = "all",
+                            running: bool = True):
+        """cv_step_reduce: the group's deferred weight gradients, the BN affine gradients of `which`
+        layers and (running=True) their running statistics, in one launch."""
+        views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
+        bns = struct_array(cv_bn, [b.cv(True) for b in views])
+        dg = ptr_array([param_grad(b.mod.weight) for b in views])
+        db = ptr_array([param_grad(b.mod.bias) for b in views])
+        nbt = ptr_array([b.mod.num_batches_tracked.data_ptr() for b in views]) if running else None
+        P.add("cv_step_reduce", defer.arr, defer.n, bns, len(views), dg, db, int(running),
+              ctypes.c_float(float(views[0].mod.momentum)), nbt)
 
     # -- programs --------------------------------------------------------------------------
     def forward_program(self, x: torch.Tensor, train: bool, eps=None, seed: int = 0, offset=None,
@@ -631,7 +683,7 @@ class Workspace:
             P.add("cv_output_loss", self.bn_dec[-1].cv(True), cur, x, n, sp.in_ch, hw, self.xhat,
                   self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
 
-    def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True):
+    def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True, defer=None):
         """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to
         dz_out [n, 2d] (zeroed + accumulated) and the decoder parameter gradients."""
         sp, n = self.spec, self.n
@@ -647,8 +699,7 @@ class Workspace:
             else:
                 P.add("cv_conv_backward_data", g, gout, c.wbwd, self.gah, ep_none())
                 xin = operand(self.ah)
-            P.add_side("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
-                       self.wg_bytes)
+            self._wgrad_call(P, "conv", g, xin, gout, param_grad(c.mod.weight), None, ("dec", li), defer)
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
         P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
@@ -658,14 +709,14 @@ class Workspace:
         gout = operand(self.gah, XF_BNBWD, self.bn_1d.cv(True), y=self.h)
         P.add("cv_linear_backward_data", lin, gout, sp.dec_lin.weight, dz_out, 1, ep_none())
 
-    def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None):
+    def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None, defer=None):
         """From d(heads) [n, 4d] to the encoder / heads parameter gradients (and dx if asked)."""
         sp, n = self.spec, self.n
         C, Hh, Wh = sp.feat
         lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
         a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
-        P.add_side("cv_linear_backward_weight", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
-                   param_grad(sp.heads[0].bias), 0, self.wg_work, self.wg_bytes)
+        self._wgrad_call(P, "linear", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
+                         param_grad(sp.heads[0].bias), ("heads",), defer)
         ep = ep_bwd(self.bn_enc[-1], self.y_enc[-1], True, stat_div=Hh * Wh)
         P.add("cv_linear_backward_data", lin, operand(dheads), sp.heads[0].weight, self.g_enc[-1], 0, ep)
         for li in range(len(sp.enc) - 1, -1, -1):
@@ -680,8 +731,7 @@ class Workspace:
                 if dx is not None:
                     P.add("cv_conv_backward_data", g, gout, c.wbwd, dx, ep_none())
                 xin = operand(x, nchw=1)
-            P.add_side("cv_conv_backward_weight", g, xin, gout, param_grad(c.mod.weight), None, 0, self.wg_work,
-                       self.wg_bytes)
+            self._wgrad_call(P, "conv", g, xin, gout, param_grad(c.mod.weight), None, ("enc", li), defer)
 
     def bn_grads_program(self, P: Program, param_grad, which: str = "all", side: bool = False):
         views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]

@@ -145,6 +145,21 @@ int cv_conv_backward_weight(const cv_conv* g, const cv_operand* in, const cv_ope
                             float* gweight, float* gbias, int split_k, float* work, size_t work_bytes,
                             cv_stream_t stream);
 
+/* Deferred weight gradients: the same contraction as cv_conv_backward_weight (split_k automatic, `work`
+ * required) but the split-K partial tiles stay in `work` and their layout is written to *defer (host
+ * struct, filled at enqueue time) instead of launching the reduction; cv_step_reduce sums them later,
+ * together with every other deferred gradient of the step, in one launch.  defer->split == 0: the
+ * launch wrote gweight / gbias directly (nothing to reduce).  `work` must stay untouched until then. */
+typedef struct cv_wgrad_defer {
+  const float* part;   /* [split][M][ntot] partial tiles                                   */
+  int split, M, N, ntot, cb, kk;
+  float* gweight;      /* += sum over splits, element (m, col = tap*cb + c) -> [m][c][tap]  */
+  float* gbias;        /* column N (if ntot > N): += row sums                              */
+} cv_wgrad_defer;
+int cv_conv_backward_weight_deferred(const cv_conv* g, const cv_operand* in, const cv_operand* gout,
+                                     float* gweight, float* gbias, float* work, size_t work_bytes,
+                                     cv_wgrad_defer* defer, cv_stream_t stream);
+
 /* ---- fully connected layers (nn.Linear heads vae.py:27-30; decoder Linear vae.py:33) ----
  * A linear layer whose input (or output) is the NCHW-flattened view of an NHWC activation with
  * `*_pix` pixels and `*_ch` channels (nn.Flatten vae.py:25 / nn.Unflatten vae.py:36).              */
@@ -166,6 +181,10 @@ size_t cv_linear_wgrad_workspace_bytes(const cv_linear* g, int split_k);
 int cv_linear_backward_weight(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
                               float* gweight, float* gbias, int split_k, float* work, size_t work_bytes,
                               cv_stream_t stream);
+
+int cv_linear_backward_weight_deferred(const cv_linear* g, const cv_operand* gout, const cv_operand* in,
+                                       float* gweight, float* gbias, float* work, size_t work_bytes,
+                                       cv_wgrad_defer* defer, cv_stream_t stream);
 
 /* Decoder Linear -> BatchNorm1d -> ReLU backward (vae.py:33-35).  da: gradient w.r.t. the ReLU
  * output in the Unflatten/NHWC order (g->out_pix, g->out_ch); h: the Linear output (BN1d input),
@@ -319,6 +338,14 @@ int cv_mi_learning_step(const cv_mlp* mlp, const float* x, int ldx, const float*
 int cv_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                  int64_t numel, const float* hyper, int64_t* step, const float* grad_scale,
                  int64_t* aux_counter, cv_stream_t stream);
+
+/* End-of-backward reduction in ONE launch (the step before the optimizer, trainer.py:482-483):
+ * the partial tiles of up to 24 deferred weight gradients (fixed split order: deterministic), the
+ * BatchNorm affine gradients dgamma = sum dz*xhat, dbeta = sum dz of up to 16 layers (when dgamma or
+ * dbeta is given; written, not accumulated) and, with running = 1, their running statistics
+ * (nn.BatchNorm*, momentum, unbiased running var; num_batches_tracked += 1 when nbt is given). */
+int cv_step_reduce(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn, float* const* dgamma,
+                   float* const* dbeta, int running, float momentum, int64_t* const* nbt, cv_stream_t stream);
 
 /* BatchNorm affine gradients from the backward sums: dgamma = sum dz*xhat, dbeta = sum dz
  * (nn.BatchNorm weight/bias grads); written (not accumulated) for up to 16 layers. */

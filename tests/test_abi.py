@@ -24,7 +24,9 @@ def test_header_declares_the_hot_path():
     fns = header_functions()
     for need in ("cv_conv_forward", "cv_conv_backward_data", "cv_conv_backward_weight", "cv_linear_forward",
                  "cv_output_loss", "cv_reparam_forward", "cv_latent_combine", "cv_ntxent", "cv_mi_forward",
-                 "cv_mi_backward", "cv_mi_learning_step", "cv_adam_step", "cv_last_error", "cv_pack_conv_weights"):
+                 "cv_mi_backward", "cv_mi_learning_step", "cv_adam_step", "cv_last_error", "cv_pack_conv_weights",
+                 "cv_latent_step", "cv_step_reduce", "cv_conv_backward_weight_deferred",
+                 "cv_linear_backward_weight_deferred"):
         assert need in fns, need
 
 
@@ -75,8 +77,9 @@ int main(void) {
   S(cv_bn) O(cv_bn, stat) O(cv_bn, C) O(cv_bn, eps)
   S(cv_operand) O(cv_operand, xf) O(cv_operand, bn)
   S(cv_epilogue) O(cv_epilogue, stat_out) O(cv_epilogue, ebn) O(cv_epilogue, erelu)
-  S(cv_conv) O(cv_conv, transposed)
-  S(cv_linear) O(cv_linear, out_ch)
+  S(cv_conv) O(cv_conv, transposed) O(cv_conv, mma)
+  S(cv_linear) O(cv_linear, out_ch) O(cv_linear, mma)
+  S(cv_wgrad_defer) O(cv_wgrad_defer, split) O(cv_wgrad_defer, kk) O(cv_wgrad_defer, gweight) O(cv_wgrad_defer, gbias)
   S(cv_conv_pack) O(cv_conv_pack, cs) O(cv_conv_pack, kw)
   S(cv_ntxent_branch)
   S(cv_mlp) S(cv_mlp_grad)
