@@ -474,17 +474,18 @@ struct StepRedArgs {
   int nbn, grads, running;
   float momentum;
 };
-constexpr int SR_E = 64;  // partial-tile elements per block (4 waves split the split range)
+constexpr int SR_E = 64;           // partial-tile elements per block: 256-byte row segments
+constexpr int SR_G = 256 / SR_E;   // split groups per element (each thread sums every SR_G-th split)
 
 __global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
-  __shared__ float red[4][SR_E];
+  __shared__ float red[SR_G][SR_E + 1];
   __shared__ double scratch[4 * 256];
   const int b = blockIdx.x, t = threadIdx.x;
   if (b < a.blk0[a.nd]) {
     int di = 0;
     while (di + 1 < a.nd && b >= a.blk0[di + 1]) ++di;
     const cv_wgrad_defer& d = a.d[di];
-    const int ol = t & 63, zg = t >> 6;
+    const int ol = t % SR_E, zg = t / SR_E;
     const long o = (long)(b - a.blk0[di]) * SR_E + ol;
     const long total = (long)d.M * d.ntot;
     const size_t sstride = (size_t)total;
@@ -492,17 +493,20 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
     if (o < total) {
       const float* p = d.part + o;
       int z = zg;
-      for (; z + 12 < d.split; z += 16) {
-        const float a0 = p[(size_t)z * sstride], a1 = p[(size_t)(z + 4) * sstride];
-        const float a2 = p[(size_t)(z + 8) * sstride], a3 = p[(size_t)(z + 12) * sstride];
-        acc += (a0 + a1) + (a2 + a3);
+      for (; z + 7 * SR_G < d.split; z += 8 * SR_G) {  // 8 independent loads in flight per thread
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(z + u * SR_G) * sstride];
+        acc += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
       }
-      for (; z < d.split; z += 4) acc += p[(size_t)z * sstride];
+      for (; z < d.split; z += SR_G) acc += p[(size_t)z * sstride];
     }
     red[zg][ol] = acc;
     __syncthreads();
     if (t < SR_E && o < total) {
-      const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < SR_G; ++g) v += red[g][t];  // fixed order: deterministic
       const int row = (int)(o / d.ntot), col = (int)(o - (long)row * d.ntot);
       if (col < d.N) {
         const int tap = col / d.cb, c = col - tap * d.cb;

@@ -38,6 +38,30 @@ __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ f32x4 g4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
+// Transposed operand staging.  Global memory holds the WGRAD A operand and every non-k-contiguous B operand
+// as rows of k with the GEMM's m / n dimension contiguous, while the LDS images are [m or n][k].  A lane
+// quad (lanes 4i..4i+3) fetches 4 consecutive k of one channel quad; quad_transpose turns that 4x4 block
+// around with two DPP quad-permutation stages, so each lane stores 4 consecutive k of ONE row as a single
+// 16-byte (bf16: 8-byte) LDS write.  16 lanes then write 16 consecutive rows of the 36-float pitch image:
+// 16 disjoint 4-bank groups.  (The round-1 scalar transposed stores walked rows 4 apart: 4- to 8-way
+// bank conflicts, SQ_LDS_BANK_CONFLICT = 87% of the LDS cycles of the weight-gradient GEMMs.)
+__device__ __forceinline__ float dpp_quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+}
+__device__ __forceinline__ float dpp_quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+}
+// lane q of a quad holds M[q][0..3]; returns M[0..3][q] (every lane of the wave must execute it)
+__device__ __forceinline__ f32x4 quad_transpose(f32x4 v, int q) {
+  const bool x = q & 1;
+  const float r0 = dpp_quad_xor1(x ? v[0] : v[1]), r1 = dpp_quad_xor1(x ? v[2] : v[3]);
+  if (x) { v[0] = r0; v[2] = r1; } else { v[1] = r0; v[3] = r1; }
+  const bool X = q & 2;
+  const float u0 = dpp_quad_xor2(X ? v[0] : v[2]), u1 = dpp_quad_xor2(X ? v[1] : v[3]);
+  if (X) { v[0] = u0; v[1] = u1; } else { v[2] = u0; v[3] = u1; }
+  return v;
+}
+
 // SoA constants: BNRELU [sc][mu][be], BNBWD [sc][c1][mu][istd][c2], each nf floats
 template <int XF>
 __host__ __device__ constexpr int soa_arrays() {
@@ -158,6 +182,9 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
   return 2 * (size_t)BM * LDK + 2 * (size_t)BN * LDK + 2 * WM * BN + nfa + nfb + nfe;
 }
 
+#ifndef CV_FAST_QTB
+#define CV_FAST_QTB 0
+#endif
 // resident waves per SIMD the register allocation must allow: the narrow-tile variants serve the
 // launches with thousands of short workgroups, where a third resident workgroup per CU removes a round
 #ifndef CV_FAST_MINW_SMALL
@@ -181,6 +208,10 @@ void gemm_kernel(const Args P) {
   constexpr bool AY = XA == CV_XF_BNBWD, BYY = XFB == CV_XF_BNBWD;
   constexpr int DBM = (OP == OP_DENSE) ? XB : DB_NCONT;    // B staging mode
   constexpr bool BKC = (DBM == DB_KCONT || DBM == DB_KPERM);
+  // quad-transposed staging of the non-k-contiguous B operand (CV_FAST_QTB=1); off by default: it makes
+  // every B load instruction touch twice the cache lines and measured slower on the forward / backward-data
+  // GEMMs, while the WGRAD A operand (worst conflicts) always uses it
+  constexpr bool QTB = (CV_FAST_QTB != 0) && !BKC;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;                       // [2][BM][LDK]
@@ -391,7 +422,7 @@ void gemm_kernel(const Args P) {
 #pragma unroll
       for (int e = 0; e < RA; ++e) {
         const int idx = t + NT * e;
-        const int mq = idx % MQ, kk = idx / MQ;
+        const int rest = idx >> 2, mq = rest % MQ, kk = 4 * (rest / MQ) + (idx & 3);  // lane quads: 4 k
         const int pix = k0 + kk, c0 = m0 + 4 * mq;
         const bool ok = pix < kend && c0 < g.cs;
         int off = pix * g.cs + c0;
@@ -425,7 +456,15 @@ void gemm_kernel(const Args P) {
         S.bm |= (ok ? 1u : 0u) << e;
       } else {
         constexpr int NQ = BN / 4;
-        const int nq = idx % NQ, kk = idx / NQ;
+        int nq, kk;
+        if constexpr (QTB) {  // lane quads: 4 consecutive k of one column quad (quad_transpose staging)
+          const int rest = idx >> 2;
+          nq = rest % NQ;
+          kk = 4 * (rest / NQ) + (idx & 3);
+        } else {  // consecutive lanes: consecutive column quads of one k (coalesced rows, scalar staging)
+          nq = idx % NQ;
+          kk = idx / NQ;
+        }
         const int col = n0 + 4 * nq, k = k0 + kk;
         bool ok = kk < BK && k < kend && col < N;
         int off = 0;
@@ -492,19 +531,14 @@ void gemm_kernel(const Args P) {
 #pragma unroll
       for (int e = 0; e < RA; ++e) {
         const int idx = t + NT * e;
-        const int mq = idx % MQ, kk = idx / MQ;
+        const int rest = idx >> 2, mq = rest % MQ, k4 = 4 * (rest / MQ), q = idx & 3;
         f32x4 v = S.a[e];
         if constexpr (XA == CV_XF_BNRELU) v = apply_xc<XA>(v, v, xa);
         if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[e], xa);
         if (!((S.am >> e) & 1u)) v = zero4();
-        if constexpr (MT == MMA_BF16) {
-          const bf16x4 h = to_bf16x4(v);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Abh[(4 * mq + j) * LDKH + kk] = h[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Ab[(4 * mq + j) * LDK + kk] = v[j];
-        }
+        v = quad_transpose(v, q);  // lane q: row 4mq + q, k = k4 .. k4 + 3
+        if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Abh + (4 * mq + q) * LDKH + k4) = to_bf16x4(v);
+        else *reinterpret_cast<f32x4*>(Ab + (4 * mq + q) * LDK + k4) = v;
       }
     }
 #pragma unroll
@@ -520,19 +554,28 @@ void gemm_kernel(const Args P) {
         }
       } else {
         constexpr int NQ = BN / 4;
-        const int nq = idx % NQ, kk = idx / NQ;
         if constexpr (XFB == CV_XF_BNRELU) v = apply_xc<XFB>(v, v, xb);
         if constexpr (XFB == CV_XF_BNBWD) v = apply_xc<XFB>(v, S.by[e], xb);
         if (!((S.bm >> e) & 1u)) v = zero4();
         if (OP == OP_WGRAD && ((S.bone >> e) & 1u)) v = f32x4{1.f, 0.f, 0.f, 0.f};
-        if (kk < BK) {
-          if constexpr (MT == MMA_BF16) {
-            const bf16x4 h = to_bf16x4(v);
+        if constexpr (QTB) {
+          const int rest = idx >> 2, nq = rest % NQ, k4 = 4 * (rest / NQ), q = idx & 3;
+          v = quad_transpose(v, q);  // lane q: column 4nq + q, k = k4 .. k4 + 3 (whole quads valid or not)
+          if (k4 < BK) {
+            if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Bbh + (4 * nq + q) * LDKH + k4) = to_bf16x4(v);
+            else *reinterpret_cast<f32x4*>(Bb + (4 * nq + q) * LDK + k4) = v;
+          }
+        } else {
+          const int nq = idx % NQ, kk = idx / NQ;
+          if (kk < BK) {
+            if constexpr (MT == MMA_BF16) {
+              const bf16x4 h = to_bf16x4(v);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Bbh[(4 * nq + j) * LDKH + kk] = h[j];
-          } else {
+              for (int j = 0; j < 4; ++j) Bbh[(4 * nq + j) * LDKH + kk] = h[j];
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Bb[(4 * nq + j) * LDK + kk] = v[j];
+              for (int j = 0; j < 4; ++j) Bb[(4 * nq + j) * LDK + kk] = v[j];
+            }
           }
         }
       }
@@ -606,11 +649,11 @@ void gemm_kernel(const Args P) {
   __syncthreads();
   if constexpr (OP == OP_WGRAD) {  // a thread's channel quads are fixed for the whole K range
     if constexpr (XA != CV_XF_NONE) {
-      const int c0 = m0 + 4 * (t % (BM / 4));
+      const int c0 = m0 + 4 * ((t >> 2) % (BM / 4));  // (the fetch's lane-quad mapping)
       xa = load_xc<XA>(cA, nfa, c0 < nfa ? c0 : 0);
     }
     if constexpr (XFB != CV_XF_NONE) {
-      const int col = n0 + 4 * (t % (BN / 4));
+      const int col = n0 + 4 * ((QTB ? (t >> 2) : t) % (BN / 4));
       xb = load_xc<XFB>(cB, nfb, col < P.N ? P.f_cb.mod(col) : 0);
     }
   }
