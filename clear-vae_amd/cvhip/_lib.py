@@ -105,6 +105,14 @@ class cv_wgrad_defer(ctypes.Structure):
                 ("kk", c_int), ("gweight", c_void_p), ("gbias", c_void_p)]
 
 
+class cv_tc_disc(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w1", "b1", "w2", "b2")] + [("zdim", c_int)]
+
+
+class cv_tc_grad(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w1", "b1", "w2", "b2")]
+
+
 class cv_ntxent_branch(ctypes.Structure):
     _fields_ = [
         ("mu", c_void_p),
@@ -221,6 +229,12 @@ _SIGS = {
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
          c_void_p, _P(cv_ntxent_branch), c_int, c_void_p, c_int, c_float, c_void_p],
     ),
+    "cv_tc_workspace_bytes": (c_size_t, [c_int]),
+    "cv_tc_forward": (
+        c_int,
+        [_P(cv_tc_disc), c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_tc_learning_step": (c_int, [_P(cv_tc_disc), c_void_p, c_int, c_void_p, c_void_p, _P(cv_tc_grad), c_void_p]),
     "cv_mi_workspace_bytes": (c_size_t, [c_int]),
     "cv_mi_forward": (
         c_int,

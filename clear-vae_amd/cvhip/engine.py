@@ -38,9 +38,27 @@ import torch.distributed as dist
 
 from . import _lib, rng
 from . import dist as cvdist
-from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
+from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch, cv_tc_disc, cv_tc_grad
 from .autograd import est_params, mlp_struct
 from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
+
+
+def disc_params(disc):
+    """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
+    None when `disc` is not Linear(z, z) -> ReLU -> Linear(z, 1) -> Sigmoid."""
+    import torch.nn as nn
+
+    mods = list(disc) if isinstance(disc, nn.Sequential) else []
+    if (len(mods) != 4 or not isinstance(mods[0], nn.Linear) or not isinstance(mods[1], nn.ReLU)
+            or not isinstance(mods[2], nn.Linear) or not isinstance(mods[3], nn.Sigmoid)):
+        return None
+    l0, l2 = mods[0], mods[2]
+    z = l0.in_features
+    if l0.out_features != z or l2.in_features != z or l2.out_features != 1 or l0.bias is None or l2.bias is None:
+        return None
+    if z > 64 or z % 2:
+        return None
+    return [l0.weight, l0.bias, l2.weight, l2.bias]
 
 
 def _dist_world():
@@ -137,6 +155,14 @@ class ClearStep:
                 return None
             if not _AdamState.supported(trainer.mi_estimator_optimizer, est_params(est)):
                 return None
+        if mode == "tc":
+            dp = disc_params(trainer.factor_cls)
+            if dp is None or dp[0].shape[1] != 2 * vae._cv_spec.d:
+                return None
+            if next(trainer.factor_cls.parameters()).device != dev:
+                return None
+            if not _AdamState.supported(trainer.factor_optimizer, dp):
+                return None
         return cls(trainer, mode)
 
     def __init__(self, trainer, mode: str):
@@ -166,13 +192,19 @@ class ClearStep:
             self.est_adam = _AdamState(trainer.mi_estimator_optimizer, self.est_arena)
             self.kind = MI_CLUBSAMPLE if type(self.est).__name__ == "CLUBSample" else MI_L1OUT
             self.learn = torch.zeros(5, dtype=torch.float32, device=self.device)
+        if mode == "tc":  # the factor discriminator plays the estimator's part: its own arena + Adam
+            self.est = trainer.factor_cls
+            self.est_arena = ParamArena(disc_params(self.est), self.device)
+            self.est_adam = _AdamState(trainer.factor_optimizer, self.est_arena)
+            self.learn = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.two_nets = mode in ("mim", "tc")
         if self.world > 1:  # DDP construction semantics: every rank starts from rank 0's weights
             cvdist.broadcast_flat(self.arena.flat)
-            if mode == "mim":
+            if self.two_nets:
                 cvdist.broadcast_flat(self.est_arena.flat)
             split = self._bucket_split()
             self.buckets = cvdist.GradBuckets(self.arena.grad, [(split, self.arena.numel), (0, split)])
-            if mode == "mim":
+            if self.two_nets:
                 self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)])
         # grads visible through p.grad (like the reference after loss.backward())
         for p in self.arena.params:
@@ -186,12 +218,14 @@ class ClearStep:
                getattr(self.vae, "_cv_precision", "fp32"))
         if self.mode == "mim":
             sig += (id(t.mi_estimator), id(t.mi_estimator_optimizer))
+        if self.mode == "tc":
+            sig += (id(t.factor_cls), id(t.factor_optimizer))
         return sig
 
     def compatible(self) -> bool:
         if self._signature() != self._sig or not self.arena.valid():
             return False
-        if self.mode == "mim" and not self.est_arena.valid():
+        if self.two_nets and not self.est_arena.valid():
             return False
         if self.anneal_expected != self.trainer.annealer.current_step:  # annealer changed by the caller
             self.anneal.fill_(self.trainer.annealer.current_step)
@@ -214,8 +248,8 @@ class ClearStep:
             self.adam.step[0] = k
         for p in self.arena.params:
             p.grad = self.arena.gview(p)
-        if self.mode == "mim":
-            st = self.trainer.mi_estimator_optimizer.state.get(self.est_arena.params[0], {})
+        if self.two_nets:
+            st = self.est_adam.opt.state.get(self.est_arena.params[0], {})
             if "step" in st:
                 k = int(float(st["step"]))
                 self.est_adam.host_steps = k
@@ -225,8 +259,8 @@ class ClearStep:
     def sync_host_state(self):
         if self.steps_since_sync:
             self.adam.sync_host(self.steps_since_sync)
-            if self.mode == "mim":
-                self.est_adam.sync_host(5 * self.steps_since_sync)
+            if self.two_nets:
+                self.est_adam.sync_host((5 if self.mode == "mim" else 1) * self.steps_since_sync)
             self.steps_since_sync = 0
 
     # ----------------------------------------------------------------------------- programs
@@ -239,7 +273,7 @@ class ClearStep:
         hp = self.hp
         d = sp.d
         pg = A.gptr
-        nslot = 6 if self.mode == "mim" else 1
+        nslot = {"mim": 6, "tc": 2}.get(self.mode, 1)
         eps_buf = torch.zeros(nslot, n, 2 * d, dtype=torch.float32, device=self.device)  # test injection
         perm_buf = torch.zeros(n, dtype=torch.int64, device=self.device)
 
@@ -299,6 +333,13 @@ class ClearStep:
                          ctypes.c_uint64(self.seed), self.offset, ws.mi_work, ws.losses.data_ptr() + 20)
                 prog.add("cv_mi_backward", self.kind, mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work, None,
                          ctypes.c_float(float(hp["lambda"])), None, None, 0, 1, None, ws.heads, ws.z, ws.dheads, d)
+        if self.mode == "tc":  # relu(log(D/(1-D))).mean() and lambda * its gradient into d(heads)
+            disc = self._disc_struct()
+            tc_work = torch.zeros(int(_lib.lib().cv_tc_workspace_bytes(2 * d)) // 4 + 4, dtype=torch.float32,
+                                  device=self.device)
+            for prog in (lat, lat_inj):
+                prog.add("cv_tc_forward", disc, ws.z, n, ctypes.c_float(float(hp["lambda"])), ws.heads, ws.dheads,
+                         d, tc_work, ws.losses.data_ptr() + 20)
         enc = Program()
         ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer)
         if dp:  # encoder bucket: its gradients and BN affine grads; every layer's running statistics
@@ -355,8 +396,37 @@ class ClearStep:
                 learn, learn_inj = make_learn_dp(False), make_learn_dp(True)
             else:
                 learn, learn_inj = make_learn(False), make_learn(True)
+        if self.mode == "tc":
+            E = self.est_arena
+            disc = self._disc_struct()
+            G = cv_tc_grad(*[E.gptr(p) for p in E.params])
+
+            def make_tc(inject: bool):
+                # trainer.py:680-699: a second train-mode forward (fresh noise) on the updated VAE, then the
+                # discriminator's BCE gradients and its Adam step (data parallel: all-reduce in between)
+                gp = Program()
+                pack_program(sp, gp, "all")  # the VAE Adam step just moved the weights
+                gp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+                ws.encoder_program(gp, X, True)
+                ws.reparam_program(gp, eps_buf[1] if inject else None, self.seed, self.offset)
+                ws.decoder_program(gp, ws.z, True, "none")
+                ws.running_program(gp, "all")
+                gp.add("cv_tc_learning_step", disc, ws.z, n, tc_work, self.learn, G)
+                ap = Program()
+                ap.add("cv_adam_step", E.flat, E.grad, self.est_adam.m, self.est_adam.v, E.numel,
+                       self.est_adam.hyper, self.est_adam.step, self.gscale if self.world > 1 else None, None)
+                if self.world > 1:
+                    return [(gp, ap)]
+                gp.extend(ap)
+                return gp
+
+            learn, learn_inj = make_tc(False), make_tc(True)
         return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, upd=upd, learn=learn,
                     fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf)
+
+    def _disc_struct(self) -> cv_tc_disc:
+        l0w, l0b, l2w, l2b = self.est_arena.params
+        return cv_tc_disc(l0w.data_ptr(), l0b.data_ptr(), l2w.data_ptr(), l2b.data_ptr(), l0w.shape[1])
 
     def _bucket_split(self):
         """Offset of the first decoder parameter in the arena (decoder grads = [split, numel))."""
@@ -405,8 +475,9 @@ class ClearStep:
 
     def _take_injections(self, G) -> bool:
         """Consume queued test noise (cvhip.rng): eps_c, eps_s for the main forward and, in CLEAR-MIM,
-        5 more pairs for the estimator forwards; plus one CLUB-S permutation."""
-        need = 2 * (6 if self.mode == "mim" else 1)
+        5 more pairs for the estimator forwards plus one CLUB-S permutation; in CLEAR-TC one more pair for
+        the discriminator step's forward."""
+        need = 2 * {"mim": 6, "tc": 2}.get(self.mode, 1)
         if rng.pending_noise() < need:
             return False
         d = self.spec.d
@@ -456,7 +527,7 @@ class ClearStep:
             G["count"] = 0
             self.graphs[n] = G
         self.adam.refresh_hyper()
-        if self.mode == "mim":
+        if self.two_nets:
             self.est_adam.refresh_hyper()
         self._load_batch(G, X, label)
         inject = self._take_injections(G)
@@ -471,7 +542,7 @@ class ClearStep:
         self.steps_since_sync += 1
         self.anneal_expected += 1
         ws = G["ws"]
-        if self.mode == "mim":
+        if self.two_nets:  # (CLEAR-MIM: the 5 learning losses; CLEAR-TC: the discriminator's BCE)
             return ws.losses, self.learn.clone()
         return ws.losses
 

@@ -10,8 +10,9 @@ replays the reference's loop literally.  Neither path computes on the CPU.
 
 Per-step scalars that the reference reads with float() every step (trainer.py:486-492, 859, 888)
 are kept on the device and copied once per epoch when the progress bar is disabled.
-The remaining trainers (CNN baselines, downstream probe, GVAE/MLVAE, CLEAR-TC) are outside the hot
-path and keep the reference's PyTorch loops.
+ClearTCVAETrainer runs fused too (mode "tc": the factor discriminator's density-ratio
+term and its BCE step as HIP kernels).  The remaining trainers (CNN baselines, downstream probe,
+GVAE/MLVAE) are outside the hot path and keep the reference's PyTorch loops.
 """
 
 from __future__ import annotations
@@ -514,8 +515,12 @@ def factor_shuffling(z: torch.Tensor, strategy: str = "permute_1"):
 
 
 class ClearTCVAETrainer(VAETrainer, _ClearEval):
-    """CLEAR-TC (trainer.py:590-778): SURVEY 8f "next" item, VAE on the HIP path via autograd,
-    factor discriminator in PyTorch."""
+    """CLEAR-TC (trainer.py:590-778).  Each step runs as one fused HIP program (cvhip.engine.ClearStep,
+    mode "tc"): the VAE step with the factor discriminator's density-ratio term relu(log(D/(1-D))).mean()
+    (cv_tc_forward), a second train-mode forward with fresh noise, and the discriminator's BCE step on
+    joint vs factor-shuffled z (cv_tc_learning_step + Adam).  Setups outside the fused contract (another
+    discriminator architecture or optimizer) run the reference's loop with the VAE on the autograd HIP
+    path and the discriminator in PyTorch."""
 
     def __init__(self, model: VAE, factor_cls: nn.Module, optimizers: dict[str, Optimizer], sim_fn: str,
                  hyperparameter: dict[str, float], verbose_period: int, device: torch.device,
@@ -527,6 +532,17 @@ class ClearTCVAETrainer(VAETrainer, _ClearEval):
         self.hyperparameter = hyperparameter
         self.annealer = LogisticAnnealer(loc=hyperparameter["loc"], scale=hyperparameter["scale"],
                                          beta=hyperparameter["beta"])
+        self._engine = None
+        self.use_fused = True
+
+    def _fused(self):
+        if not self.use_fused:
+            return None
+        from cvhip.engine import ClearStep
+
+        if self._engine is None or not self._engine.compatible():
+            self._engine = ClearStep.build(self, mode="tc")
+        return self._engine
 
     def fit(self, epochs: int, train_loader: DataLoader, valid_loader: None | DataLoader = None):
         factor_d_losses = []
@@ -542,11 +558,27 @@ class ClearTCVAETrainer(VAETrainer, _ClearEval):
         vae.train()
         cls.train()
         hp = self.hyperparameter
+        engine = self._fused()
         log = []
         with tqdm(dataloader, unit="batch", mininterval=0, disable=not verbose) as bar:
             bar.set_description(f"Epoch {epoch_id}")
             for batch in bar:
                 X, label = _batch(batch, self.device, self.transform)
+                if engine is not None and engine.accepts(X):
+                    if getattr(self, "_resync", False):
+                        engine.resync_from_host()
+                        self._resync = False
+                    losses, fl = engine.step(X, label)
+                    self.annealer.step()
+                    log.append(fl)
+                    if verbose:
+                        v = losses.tolist()
+                        bar.set_postfix(factor_cls_loss=float(fl), recontr_loss=v[0], kl_c=v[1], kl_s=v[2],
+                                        c_loss=v[3], mi_loss=v[5])
+                    continue
+                if engine is not None:
+                    engine.sync_host_state()
+                    self._resync = True
                 X_hat, lp, z = vae(X, explicit=True)
                 self.optimizer.zero_grad()
                 rec, kl_c, kl_s = vae_loss(X_hat, X, **lp)
@@ -572,8 +604,10 @@ class ClearTCVAETrainer(VAETrainer, _ClearEval):
                 if verbose:
                     bar.set_postfix(factor_cls_loss=float(factor_loss), recontr_loss=float(rec), kl_c=float(kl_c),
                                     kl_s=float(kl_s), c_loss=float(c_loss), mi_loss=float(mi_loss))
+        if engine is not None:
+            engine.sync_host_state()
         if log:
-            factor_d_losses.extend(torch.cat(log).tolist())
+            factor_d_losses.extend(torch.cat([t.reshape(1) for t in log]).tolist())
 
     def evaluate(self, dataloader, verbose, epoch_id):
         self.factor_cls.eval()

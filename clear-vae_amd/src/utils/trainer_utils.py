@@ -74,8 +74,11 @@ def get_clearvae_trainer(beta, ps, vae_lr, z_dim, alpha, temperature, device, va
 
 
 def get_cleartcvae_trainer(beta, la, vae_lr, factor_cls_lr, z_dim, alpha, temperature, device,
-                           vae_arch: str = "VAE", in_channel: int = 1, verbose_period: int = 5):
+                           vae_arch: str = "VAE", in_channel: int = 1, verbose_period: int = 5,
+                           precision: str = "fp32"):
+    """(trainer_utils.py:119-157); `precision` as in get_clearvae_trainer."""
     vae = _resolve(vae_arch)(total_z_dim=z_dim, in_channel=in_channel).to(device)
+    set_precision(vae, precision)
     factor_cls = nn.Sequential(nn.Linear(z_dim, z_dim), nn.ReLU(), nn.Linear(z_dim, 1), nn.Sigmoid()).to(device)
     vae_opt = torch.optim.Adam(vae.parameters(), lr=vae_lr)
     fac_opt = torch.optim.Adam(factor_cls.parameters(), lr=factor_cls_lr)

@@ -330,6 +330,27 @@ int cv_mi_learning_step(const cv_mlp* mlp, const float* x, int ldx, const float*
                         float* exp_avg, float* exp_avg_sq, int64_t numel, const float* hyper,
                         int64_t* step, cv_stream_t stream);
 
+/* ---- CLEAR-TC factor discriminator (trainer.py:573-699, trainer_utils.py:133-138) ----
+ * factor_cls = Linear(z, z) -> ReLU -> Linear(z, 1) -> Sigmoid, Linear weights [out][in]; z <= 64, even. */
+typedef struct cv_tc_disc {
+  const float *w1, *b1, *w2, *b2;
+  int zdim;
+} cv_tc_disc;
+typedef struct cv_tc_grad {
+  float *w1, *b1, *w2, *b2;
+} cv_tc_grad;
+size_t cv_tc_workspace_bytes(int zdim);
+/* mi_out[0] = relu(log(d / (1 - d))).mean(), d = factor_cls(z) (trainer.py:664-665), z [n][zdim].  With
+ * dheads != NULL also accumulates the gradient of lam * mi_loss into d(heads) through
+ * z = mu + eps*exp(logvar/2) (heads / dheads [n][4d] = mu_c | lv_c | mu_s | lv_s, d = zdim/2). */
+int cv_tc_forward(const cv_tc_disc* D, const float* z, int n, float lam, const float* heads, float* dheads, int d,
+                  void* work, float* mi_out, cv_stream_t stream);
+/* The discriminator's step loss (trainer.py:683-694): BCE of factor_cls on z (target 1) and on
+ * factor_shuffling(z) "permute_1" (target 0); loss_out[0] and the parameter gradients (overwritten).
+ * The optimizer update is cv_adam_step on the discriminator's arena. */
+int cv_tc_learning_step(const cv_tc_disc* D, const float* z, int n, void* work, float* loss_out,
+                        const cv_tc_grad* g, cv_stream_t stream);
+
 /* ---- Adam (torch.optim.Adam foreach semantics) over a flat fp32 arena ----
  * hyper: device float[8] = lr, beta1, beta2, eps, weight_decay; step: device int64[2] =
  * (steps taken, arrival counter = 0).  grad_scale (device float or NULL) multiplies the gradient

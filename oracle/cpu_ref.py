@@ -9,9 +9,12 @@ written against torch.nn.functional so that it runs in fp32 or fp64 on the host.
   logsumexp / snn_loss         code/src/losses.py:87-95, 129-137
   contrastive_loss             code/src/losses.py:98-126
   CLUBSample / L1OutUB         code/src/models/mi_estimator.py:108-198
+  factor discriminator, factor_shuffling, CLEAR-TC step
+                               code/src/utils/trainer_utils.py:133-138, code/src/trainer.py:573-699
   LogisticAnnealer             code/src/trainer.py:22-38
   CLEARVAETrainer step         code/src/trainer.py:447-484
   ClearMIMVAETrainer step      code/src/trainer.py:842-888
+  ClearTCVAETrainer step       code/src/trainer.py:648-699
 with the reparameterisation noise and the CLUB-S permutation passed in explicitly.
 Gradients come from torch autograd on the CPU.
 
@@ -143,6 +146,15 @@ def det_mlp(d: int, hidden_size: int, seed: int = 2) -> dict:
         out[f"{net}.2.weight"] = rng.uniform(-b2, b2, (d, h))
         out[f"{net}.2.bias"] = rng.uniform(-b2, b2, (d,))
     return out
+
+
+def det_disc(z_total: int, seed: int = 3) -> dict:
+    """Deterministic factor-discriminator weights: nn.Sequential(Linear(z, z), ReLU, Linear(z, 1), Sigmoid)
+    (trainer_utils.py:133-138), Linear bound 1/sqrt(fan_in)."""
+    rng = np.random.default_rng(seed)
+    b = 1.0 / math.sqrt(z_total)
+    return {"0.weight": rng.uniform(-b, b, (z_total, z_total)), "0.bias": rng.uniform(-b, b, (z_total,)),
+            "2.weight": rng.uniform(-b, b, (1, z_total)), "2.bias": rng.uniform(-b, b, (1,))}
 
 
 # ----------------------------------------------------------------------------- functional model
@@ -346,3 +358,46 @@ def mim_step(P, M, x, label, eps_c, eps_s, perm, arch, hp, kind="CLUBSample", si
     grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
     return {"xhat": xhat, "z": z, **lp, "rec": rec, "kl_c": kl_c, "kl_s": kl_s, "c_loss": c, "mi": mi,
             "loss": loss, "grads": {k: g for k, g in zip(params, grads)}}
+
+
+# ----------------------------------------------------------------------------- CLEAR-TC
+
+
+def disc_forward(D, z):
+    """factor_cls(z) (trainer_utils.py:133-138): [n, 1] probabilities."""
+    return torch.sigmoid(F.linear(F.relu(F.linear(z, D["0.weight"], D["0.bias"])), D["2.weight"], D["2.bias"]))
+
+
+def factor_shuffling(z):
+    """strategy "permute_1" (trainer.py:573-587): z_s rolled up by one row."""
+    d = z.shape[1] // 2
+    return torch.cat([z[:, :d], torch.cat([z[1:, d:], z[:1, d:]], dim=0)], dim=1)
+
+
+def tc_mi_loss(D, z):
+    """F.relu(torch.log(d_score / (1 - d_score))).mean() (trainer.py:664-665)."""
+    d = disc_forward(D, z)
+    return F.relu(torch.log(d / (1 - d))).mean()
+
+
+def tc_step(P, D, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0):
+    """The VAE half of one ClearTCVAETrainer step (trainer.py:654-677): losses and VAE grads (the
+    discriminator's grads of this backward are discarded by factor_optimizer.zero_grad, :682)."""
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True)
+    rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
+    c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
+    mi = tc_mi_loss(D, z)
+    w = anneal_weight(step, hp["beta"], hp.get("loc", 0), hp.get("scale", 1))
+    loss = rec + w * kl_c + w * kl_s + hp["alpha"] * c + hp["lambda"] * mi
+    params = {k: v for k, v in P.items() if isinstance(v, torch.Tensor) and v.requires_grad}
+    grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
+    return {"xhat": xhat, "z": z, **lp, "rec": rec, "kl_c": kl_c, "kl_s": kl_s, "c_loss": c, "mi": mi,
+            "loss": loss, "grads": {k: g for k, g in zip(params, grads)}}
+
+
+def tc_factor_loss(D, z):
+    """nn.BCELoss()(cat[factor_cls(z), factor_cls(factor_shuffling(z))], cat[1, 0]) (trainer.py:682-694);
+    z is detached."""
+    dj = disc_forward(D, z)
+    dm = disc_forward(D, factor_shuffling(z))
+    return F.binary_cross_entropy(torch.cat([dj, dm], dim=0), torch.cat([torch.ones_like(dj), torch.zeros_like(dm)]))

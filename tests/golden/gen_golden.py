@@ -1,6 +1,7 @@
 """Generate the golden fixtures tests/golden/*.npz from the REAL reference (development container only).
 
-Runs one real `CLEARVAETrainer._train` / `ClearMIMVAETrainer._train` step of scotsun/clear-vae
+Runs one real `CLEARVAETrainer._train` / `ClearMIMVAETrainer._train` / `ClearTCVAETrainer._train` step of
+scotsun/clear-vae
 (imported read-only from /root/reference/code, never copied) in float64 on the CPU, with:
   * weights from oracle.cpu_ref.det_state / det_mlp (numpy PCG64, so no weights are stored),
   * inputs from oracle.cpu_ref.det_inputs (seeded; a checksum of them is stored to catch drift),
@@ -52,13 +53,15 @@ CASES = [
     ("vae_n64_mim_l1out", "VAE", 16, 1, 64, 10, "mim", "cosine", None, "L1OutUB", False),
     ("vae64_n16_cosine_ps1", "VAE64", 64, 3, 16, 4, "clear", "cosine", True, None, True),
     ("vae64_n16_mim_club", "VAE64", 64, 3, 16, 4, "mim", "cosine", None, "CLUBSample", False),
+    ("vae_n64_tc", "VAE", 16, 1, 64, 10, "tc", "cosine", None, None, False),
+    ("vae64_n16_tc", "VAE64", 64, 3, 16, 4, "tc", "cosine", None, None, False),
 ]
 
 HP = {
     "VAE": {"temperature": 0.1, "alpha": 100.0, "beta": 1 / 8, "loc": 0, "scale": 1, "lambda": 3.0,
-            "lr": 5e-4, "est_lr": 2e-3},
+            "lr": 5e-4, "est_lr": 2e-3, "factor_lr": 1e-3},
     "VAE64": {"temperature": 0.1, "alpha": 100.0, "beta": 1 / 32, "loc": 0, "scale": 1, "lambda": 3.0,
-              "lr": 3e-5, "est_lr": 2e-3},
+              "lr": 3e-5, "est_lr": 2e-3, "factor_lr": 1e-3},
 }
 
 
@@ -135,6 +138,43 @@ def run_case(case):
             tr = T.CLEARVAETrainer(model, opt, sim_fn, hyper, 1, torch.device("cpu"))
             with injected(noise, torch.tensor(perm)):
                 tr._train([(X, L)], False, 0)
+        elif mode == "tc":
+            # factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138), deterministic weights
+            d = z // 2
+            disc = torch.nn.Sequential(torch.nn.Linear(z, z), torch.nn.ReLU(), torch.nn.Linear(z, 1),
+                                       torch.nn.Sigmoid()).double()
+            disc.load_state_dict({k: torch.as_tensor(v) for k, v in R.det_disc(z).items()}, strict=True)
+            calls = []
+            orig_disc_fwd = disc.forward
+
+            def disc_rec(zin):
+                o = orig_disc_fwd(zin)
+                calls.append((zin.detach().clone(), o.detach().clone()))
+                return o
+
+            disc.forward = disc_rec
+            gen = np.random.default_rng(6)
+            a, b = gen.standard_normal((n, d)), gen.standard_normal((n, d))  # the second forward's noise
+            extra.append((a, b))
+            noise += [torch.tensor(a), torch.tensor(b)]
+            fopt = torch.optim.Adam(disc.parameters(), lr=hp["factor_lr"])
+            hyper = {k: hp[k] for k in ("temperature", "alpha", "beta", "loc", "scale", "lambda")}
+            tr = T.ClearTCVAETrainer(model, disc, {"vae_optim": opt, "factor_optim": fopt}, sim_fn, hyper, 1,
+                                     torch.device("cpu"))
+            fl = []
+            with injected(noise, torch.tensor(perm)):
+                tr._train([(X, L)], False, 0, fl)
+            assert len(calls) == 3  # d_score (VAE step), joint and marginal scores (factor step)
+            dsc = calls[0][1]
+            out["mi"] = np.float64(torch.relu(torch.log(dsc / (1 - dsc))).mean())
+            out["z"] = calls[0][0].numpy()
+            out["z2"] = calls[1][0].numpy()
+            out["factor_loss"] = np.float64(fl[0])
+            for k, v in disc.state_dict().items():
+                out["disc_after__" + k] = v.numpy()
+            for k, v in disc.named_parameters():
+                out["disc_grad__" + k] = v.grad.detach().numpy()
+            out["extra_noise"] = np.stack([np.stack(p) for p in extra])  # [1, 2, n, d]
         else:
             d = z // 2
             M = R.det_mlp(d, z)

@@ -59,6 +59,11 @@ def oracle_step(fx: dict, dtype=torch.float64) -> dict:
     if mode == "clear":
         o = R.clear_step(P, X, L, Ec, Es, arch, hp, m["sim_fn"])
         out["s_loss"] = float(o["s_loss"].detach())
+    elif mode == "tc":
+        D = R.to_torch(R.det_disc(m["z"]), dtype)
+        o = R.tc_step(P, D, X, L, Ec, Es, arch, hp, m["sim_fn"])
+        out["mi"] = float(o["mi"].detach())
+        out["z"] = o["z"].detach().numpy()
     else:
         M = R.to_torch(R.det_mlp(m["z"] // 2, m["z"]), dtype)
         o = R.mim_step(P, M, X, L, Ec, Es, torch.tensor(perm), arch, hp, m["estimator"], m["sim_fn"])
@@ -90,6 +95,22 @@ def oracle_step(fx: dict, dtype=torch.float64) -> dict:
             learn.append(float(ll))
         out["mi_learning"] = np.array(learn)
         out["est_after"] = {k: v.detach().numpy() for k, v in M.items()}
+    if mode == "tc":
+        # factor step (trainer.py:680-699): a second train-mode forward with fresh noise on the updated VAE,
+        # BCE of the discriminator on joint / factor-shuffled z, torch Adam on the discriminator
+        a, b = fx["extra_noise"][0]
+        with torch.no_grad():
+            _, _, z2 = R.vae_forward(P, X, torch.tensor(a, dtype=dtype), torch.tensor(b, dtype=dtype), arch, True)
+        Dp = list(D.values())
+        for p_ in Dp:
+            p_.grad = None
+        fl = R.tc_factor_loss(D, z2.detach())
+        fl.backward()
+        out["z2"] = z2.numpy()
+        out["factor_loss"] = float(fl.detach())
+        out["disc_grad"] = {k: v.grad.detach().numpy().copy() for k, v in D.items()}
+        torch.optim.Adam(Dp, lr=hp["factor_lr"]).step()
+        out["disc_after"] = {k: v.detach().numpy() for k, v in D.items()}
     out["after"] = {k: p.detach().numpy() for k, p in params.items()}
     out["buffers"] = {k: v.detach().numpy() for k, v in P.items()
                       if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}

@@ -26,7 +26,7 @@ def test_header_declares_the_hot_path():
                  "cv_output_loss", "cv_reparam_forward", "cv_latent_combine", "cv_ntxent", "cv_mi_forward",
                  "cv_mi_backward", "cv_mi_learning_step", "cv_adam_step", "cv_last_error", "cv_pack_conv_weights",
                  "cv_latent_step", "cv_step_reduce", "cv_conv_backward_weight_deferred",
-                 "cv_linear_backward_weight_deferred"):
+                 "cv_linear_backward_weight_deferred", "cv_tc_forward", "cv_tc_learning_step"):
         assert need in fns, need
 
 
@@ -83,6 +83,7 @@ int main(void) {
   S(cv_conv_pack) O(cv_conv_pack, cs) O(cv_conv_pack, kw)
   S(cv_ntxent_branch)
   S(cv_mlp) S(cv_mlp_grad)
+  S(cv_tc_disc) O(cv_tc_disc, zdim) S(cv_tc_grad)
   return 0;
 }
 """

@@ -42,6 +42,15 @@ def _estimator(fx):
     return est
 
 
+def _disc(fx):
+    from oracle import cpu_ref as R
+
+    z = fx["meta"]["z"]
+    disc = torch.nn.Sequential(torch.nn.Linear(z, z), torch.nn.ReLU(), torch.nn.Linear(z, 1), torch.nn.Sigmoid()).cuda()
+    disc.load_state_dict({k: torch.tensor(v, dtype=torch.float32) for k, v in R.det_disc(z).items()})
+    return disc
+
+
 def _close(a, ref, floor=1e-3):
     return abs(float(a) - float(ref)) <= TOL * max(abs(float(ref)), floor)
 
@@ -82,6 +91,12 @@ def test_module_outputs_vs_golden(name):
         with torch.no_grad():
             s = contrastive_loss(lp["mu_s"], lp["logvar_s"], L, m["sim_fn"], m["hp"]["temperature"], ps=m["ps"])
         assert _close(s, fx["s_loss_raw"]), (float(s), float(fx["s_loss_raw"]))
+    elif m["mode"] == "tc":
+        assert G.rel(z.cpu().numpy(), fx["z"]) < TOL
+        with torch.no_grad():
+            dsc = _disc(fx)(z)
+            mi = torch.relu(torch.log(dsc / (1 - dsc))).mean()
+        assert abs(float(mi) - float(fx["mi"])) <= TOL * max(abs(float(fx["mi"])), 1.0), (float(mi), float(fx["mi"]))
     else:
         assert G.rel(z.cpu().numpy(), fx["z"]) < TOL
         est = _estimator(fx)
@@ -96,7 +111,7 @@ def test_module_outputs_vs_golden(name):
 def test_fused_step_vs_golden(name):
     from cvhip import rng
     from cvhip.engine import ClearStep
-    from src.trainer import ClearMIMVAETrainer, CLEARVAETrainer
+    from src.trainer import ClearMIMVAETrainer, ClearTCVAETrainer, CLEARVAETrainer
 
     fx = G.load(name)
     m = fx["meta"]
@@ -110,6 +125,14 @@ def test_fused_step_vs_golden(name):
     if m["mode"] == "clear":
         tr = CLEARVAETrainer(vae, opt, m["sim_fn"], hp, 1, torch.device("cuda"))
         eng = ClearStep.build(tr, "clear")
+    elif m["mode"] == "tc":
+        disc = _disc(fx)
+        fopt = torch.optim.Adam(disc.parameters(), lr=hp["factor_lr"])
+        tr = ClearTCVAETrainer(vae, disc, {"vae_optim": opt, "factor_optim": fopt}, m["sim_fn"], hp, 1,
+                               torch.device("cuda"))
+        eng = ClearStep.build(tr, "tc")
+        for a, b in fx["extra_noise"]:
+            noise += [torch.tensor(a, dtype=torch.float32), torch.tensor(b, dtype=torch.float32)]
     else:
         est = _estimator(fx)
         eopt = torch.optim.Adam(est.parameters(), lr=hp["est_lr"])
@@ -130,6 +153,15 @@ def test_fused_step_vs_golden(name):
         assert _close(losses[i], fx[k]), (k, float(losses[i]), float(fx[k]))
     if m["mode"] == "clear":
         assert _close(losses[4], fx["s_loss_raw"]), (float(losses[4]), float(fx["s_loss_raw"]))
+    elif m["mode"] == "tc":
+        assert abs(float(losses[5]) - float(fx["mi"])) <= TOL * max(abs(float(fx["mi"])), 1.0)
+        # the discriminator's step runs on z of a second forward through the post-Adam VAE, whose
+        # knife-edge / noise-gradient Adam steps (see above) move z at ~1e-5: 1e-3 on its results
+        assert abs(float(learn[0]) - float(fx["factor_loss"])) <= 1e-3 * abs(float(fx["factor_loss"]))
+        dprels = []
+        for k, p in disc.named_parameters():
+            dprels.append(G.rel(p.detach().double().cpu().numpy(), fx["disc_after__" + k]))
+        assert max(dprels) < 1e-3, dprels
     else:
         assert abs(float(losses[5]) - float(fx["mi"])) <= TOL * max(abs(float(fx["mi"])), 1.0)
         ll = learn.cpu().numpy()
@@ -159,7 +191,7 @@ def test_fused_step_vs_golden(name):
     assert prels[len(prels) // 2][0] < 1e-5, prels[-3:]
     assert prels[-1][0] < 5e-3, prels[-3:]
     # BatchNorm running statistics after the step's train-mode forwards (1, or 6 in CLEAR-MIM)
-    btol = 1e-4 if m["mode"] == "clear" else 1e-3
+    btol = 1e-4 if m["mode"] == "clear" else 1e-3  # (MIM / TC: forwards after the Adam step)
     for k, v in tr.model.state_dict().items():
         if k.endswith(("running_mean", "running_var")):
             assert G.rel(v.double().cpu().numpy(), fx["buf__" + k]) < btol, k

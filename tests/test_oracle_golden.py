@@ -23,7 +23,7 @@ def test_fixture_set_complete():
     have = set(G.names())
     for need in ("vae_n64_cosine_ps1", "vae_n64_cosine_ps0", "vae_n64_l2_ps1", "vae_n64_jeffrey_ps1",
                  "vae_n512_cosine_ps1", "vae_n64_mim_club", "vae_n64_mim_l1out", "vae64_n16_cosine_ps1",
-                 "vae64_n16_mim_club"):
+                 "vae64_n16_mim_club", "vae_n64_tc", "vae64_n16_tc"):
         assert need in have, need
 
 
@@ -66,7 +66,7 @@ def test_adam_update_and_buffers(case):
         assert G.rel(ours, ref) < 1e-9 or np.abs(ours - ref).max() <= 1e-4 * lr, (name, k)
     # CLEAR-MIM's 5 extra forwards run on the post-Adam weights, so the running means inherit the
     # noise-level bias steps above (the conv bias shifts the BN input mean one-for-one)
-    btol = 1e-9 if fx["meta"]["mode"] == "clear" else 1e-7
+    btol = 1e-9 if fx["meta"]["mode"] == "clear" else 1e-7  # (CLEAR-TC: one extra forward, as MIM)
     for k, b in o["buffers"].items():
         assert G.rel(b, fx["buf__" + k]) < btol, (name, k)
     if fx["meta"]["mode"] == "mim":
@@ -74,3 +74,17 @@ def test_adam_update_and_buffers(case):
                                                                                        fx["mi_learning"])
         for k, v in o["est_after"].items():
             assert G.rel(v, fx["est_after__" + k]) < 1e-9, (name, k)
+
+
+def test_clear_tc_factor_step(case):
+    """CLEAR-TC's factor-discriminator step (trainer.py:680-699): z of the second forward, the BCE value,
+    the discriminator gradients and its parameters after torch Adam."""
+    name, fx, o = case
+    if fx["meta"]["mode"] != "tc":
+        pytest.skip("CLEAR-TC cases only")
+    assert G.rel(o["z2"], fx["z2"]) < 1e-7  # post-Adam weights: the bias-noise steps above
+    assert abs(o["factor_loss"] - float(fx["factor_loss"])) <= 1e-7 * abs(float(fx["factor_loss"]))
+    for k, g in o["disc_grad"].items():
+        assert G.rel(g, fx["disc_grad__" + k]) < 1e-6, (name, k)
+    for k, v in o["disc_after"].items():
+        assert G.rel(v, fx["disc_after__" + k]) < 1e-9, (name, k)
