@@ -33,6 +33,7 @@ STAT_NONE, STAT_FWD, STAT_BWD = 0, 1, 2
 SIM = {"cosine": 0, "l2": 1, "modified_l2": 2, "jeffrey": 3, "mahalanobis": 4}
 MI_NONE, MI_CLUBSAMPLE, MI_L1OUT = 0, 1, 2
 MMA_FP32, MMA_BF16 = 0, 1  # CV_MMA_*
+GROUP = {"MLVAE": 0, "GVAE": 1}  # CV_GROUP_*
 PRECISION = {"fp32": MMA_FP32, "bf16": MMA_BF16}
 
 
@@ -235,6 +236,22 @@ _SIGS = {
         [_P(cv_tc_disc), c_void_p, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     ),
     "cv_tc_learning_step": (c_int, [_P(cv_tc_disc), c_void_p, c_int, c_void_p, c_void_p, _P(cv_tc_grad), c_void_p]),
+    "cv_group_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "cv_group_forward": (
+        c_int,
+        [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+         c_void_p, c_int, c_uint64, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_group_backward": (
+        c_int,
+        [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_group_evidence_backward": (
+        c_int,
+        [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+         c_void_p],
+    ),
     "cv_mi_workspace_bytes": (c_size_t, [c_int]),
     "cv_mi_forward": (
         c_int,

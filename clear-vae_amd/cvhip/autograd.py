@@ -13,7 +13,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib, rng
-from ._lib import MI_CLUBSAMPLE, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
+from ._lib import GROUP, MI_CLUBSAMPLE, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch
 from .plan import Program, Workspace, ensure_arena, pack_program
 
 
@@ -192,6 +192,62 @@ class SampleFn(torch.autograd.Function):
         return dmu, dlv
 
 
+# ----------------------------------------------------------------------------- group evidence
+
+
+def _group_offsets(n: int, d: int):
+    """int32 offsets of m / order / start and the fp32 offset of the group rows in a cv_group_forward
+    workspace (include/clearvae.h)."""
+    order = 16 + 2 * n
+    start = 16 + 3 * n
+    rows = ((64 + 16 * n + 4) + 15) // 16 * 4
+    return order, start, rows
+
+
+class GroupEvidenceFn(torch.autograd.Function):
+    """accumulate_group_evidence (vae.py:159-190): the group rows (mu_g, logvar_g) [m, d], segmented by
+    label on the device (cv_group_forward).  `meta` (a dict) receives the groups as the reference's
+    {label: member indices} dict; building it is the one host read of the call."""
+
+    @staticmethod
+    def forward(ctx, mu_c, logvar_c, label, mode, meta):
+        if mode not in GROUP:
+            raise NotImplementedError("only support using MLVAE or GVAE")
+        mu, lv = _f32c(mu_c), _f32c(logvar_c)
+        lab = label.reshape(-1).to(device=mu.device, dtype=torch.int64).contiguous()
+        n, d = mu.shape
+        work = torch.zeros(int(_lib.lib().cv_group_workspace_bytes(n, d)) // 4 + 4, dtype=torch.float32,
+                           device=mu.device)
+        _lib.call("cv_group_forward", GROUP[mode], mu.data_ptr(), lv.data_ptr(), d, lab.data_ptr(), n, d,
+                  work.data_ptr(), None, None, None, 0, None, 0, 0, None, None, _lib.stream_handle())
+        o_order, o_start, o_rows = _group_offsets(n, d)
+        iw = work.view(torch.int32)
+        host = torch.cat([iw[:1], iw[o_order:o_order + n], iw[o_start:o_start + n + 1]]).cpu()
+        m = int(host[0])
+        order, start = host[1:1 + n], host[1 + n:]
+        lab_h = lab.cpu()
+        order_d = iw[o_order:o_order + n].long()
+        meta["groups"] = {int(lab_h[int(order[int(start[g])])]): order_d[int(start[g]):int(start[g + 1])]
+                          for g in range(m)}
+        rows = work[o_rows:o_rows + n * 2 * d].view(n, 2 * d)
+        ctx.save_for_backward(mu, lv, work)
+        ctx.meta = (GROUP[mode], n, d, m)
+        return rows[:m, :d].clone(), rows[:m, d:].clone()
+
+    @staticmethod
+    def backward(ctx, g_mu, g_lv):
+        mu, lv, work = ctx.saved_tensors
+        mode, n, d, m = ctx.meta
+        gm = _f32c(g_mu) if g_mu is not None else None
+        gl = _f32c(g_lv) if g_lv is not None else None
+        dmu = torch.empty(n, d, dtype=torch.float32, device=mu.device)
+        dlv = torch.empty_like(dmu)
+        _lib.call("cv_group_evidence_backward", mode, mu.data_ptr(), lv.data_ptr(), d, work.data_ptr(), n, d,
+                  gm.data_ptr() if gm is not None else None, gl.data_ptr() if gl is not None else None,
+                  dmu.data_ptr(), dlv.data_ptr(), d, _lib.stream_handle())
+        return dmu, dlv, None, None, None
+
+
 # ----------------------------------------------------------------------------- losses
 
 
@@ -219,10 +275,12 @@ class VaeLossFn(torch.autograd.Function):
         ms, lds = _rows(mu_s)
         ls, _ = _rows(lv_s)
         assert lc.stride(0) == ldc and ls.stride(0) == lds
-        _lib.call("cv_kl", mc.data_ptr(), lc.data_ptr(), ldc, n, mc.shape[1], out.data_ptr() + 4, None, None, None,
-                  0, 0, s)
-        _lib.call("cv_kl", ms.data_ptr(), ls.data_ptr(), lds, n, ms.shape[1], out.data_ptr() + 8, None, None, None,
-                  0, 0, s)
+        # (each KL over its own rows: GVAE / ML-VAE pass the m group rows as mu_c / logvar_c)
+        assert lc.shape == mc.shape and ls.shape == ms.shape
+        _lib.call("cv_kl", mc.data_ptr(), lc.data_ptr(), ldc, mc.shape[0], mc.shape[1], out.data_ptr() + 4, None,
+                  None, None, 0, 0, s)
+        _lib.call("cv_kl", ms.data_ptr(), ls.data_ptr(), lds, ms.shape[0], ms.shape[1], out.data_ptr() + 8, None,
+                  None, None, 0, 0, s)
         ctx.save_for_backward(xh, xx, mc, lc, ms, ls)
         return out[0], out[1], out[2]
 
@@ -244,7 +302,7 @@ class VaeLossFn(torch.autograd.Function):
             g = _f32c(gk.reshape(1))
             dm = torch.empty(m.shape, dtype=torch.float32, device=m.device)
             dl = torch.empty_like(dm)
-            _lib.call("cv_kl", m.data_ptr(), l.data_ptr(), m.stride(0), n, m.shape[1], None, g.data_ptr(),
+            _lib.call("cv_kl", m.data_ptr(), l.data_ptr(), m.stride(0), m.shape[0], m.shape[1], None, g.data_ptr(),
                       dm.data_ptr(), dl.data_ptr(), dm.stride(0), 0, s)
             res[im], res[il] = dm, dl
         return tuple(res)

@@ -10,7 +10,10 @@ calls over device-resident buffers:
   Adam on the flat parameter arena (+ LogisticAnnealer step on the device)
 
 For CLEAR-MIM the 5 estimator updates follow (each: a train-mode forward for BN statistics and z,
-then one fused learning-loss + Adam kernel on the estimator arena).
+then one fused learning-loss + Adam kernel on the estimator arena).  For the GVAE / ML-VAE baselines
+(HierarchicalVAETrainer._train, code/src/trainer.py:326-353; mode "group") the reparameterisation is the
+label-segmented group evidence (cv_group_forward: no host round trip for the groups) and the latent
+terms are cv_group_backward (kl_c over the groups, the B/m adjustment of rec and kl_s).
 
 The first step at a new batch size runs eagerly (it also loads the code objects); the second is
 captured into a torch.cuda.CUDAGraph and every later step replays it.  Step-varying scalars (RNG
@@ -38,7 +41,7 @@ import torch.distributed as dist
 
 from . import _lib, rng
 from . import dist as cvdist
-from ._lib import MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch, cv_tc_disc, cv_tc_grad
+from ._lib import GROUP, MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch, cv_tc_disc, cv_tc_grad
 from .autograd import est_params, mlp_struct
 from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
 
@@ -144,8 +147,10 @@ class ClearStep:
             return None
         if not _AdamState.supported(trainer.optimizer, arena.params):
             return None
-        sim = trainer.sim_fn
-        if sim not in SIM:
+        if mode == "group":
+            if getattr(vae, "mode", None) not in GROUP or vae._cv_spec.d > 64:
+                return None
+        elif trainer.sim_fn not in SIM:
             raise ValueError("unimplemented similarity measure.")
         if mode == "mim":
             from src.models.mi_estimator import CLUBSample, L1OutUB
@@ -175,7 +180,8 @@ class ClearStep:
         self.adam = _AdamState(trainer.optimizer, self.arena)
         hp = trainer.hyperparameter
         self.hp = dict(hp)
-        self.sim = SIM[trainer.sim_fn]
+        self.sim = SIM[trainer.sim_fn] if mode != "group" else 0
+        self.group_mode = GROUP[self.vae.mode] if mode == "group" else None
         self.anneal = torch.tensor([trainer.annealer.current_step], dtype=torch.int64, device=self.device)
         self.anneal_expected = trainer.annealer.current_step
         # the shared (device, seed) Philox counter: engine rebuilds and the module path (evaluate, fallback
@@ -214,8 +220,9 @@ class ClearStep:
     # ----------------------------------------------------------------------------- bookkeeping
     def _signature(self):
         t = self.trainer
-        sig = (id(t.optimizer), t.sim_fn, tuple(sorted((k, str(v)) for k, v in t.hyperparameter.items())),
-               getattr(self.vae, "_cv_precision", "fp32"))
+        sig = (id(t.optimizer), getattr(t, "sim_fn", None),
+               tuple(sorted((k, str(v)) for k, v in t.hyperparameter.items())),
+               getattr(self.vae, "_cv_precision", "fp32"), getattr(self.vae, "mode", None))
         if self.mode == "mim":
             sig += (id(t.mi_estimator), id(t.mi_estimator_optimizer))
         if self.mode == "tc":
@@ -276,6 +283,11 @@ class ClearStep:
         nslot = {"mim": 6, "tc": 2}.get(self.mode, 1)
         eps_buf = torch.zeros(nslot, n, 2 * d, dtype=torch.float32, device=self.device)  # test injection
         perm_buf = torch.zeros(n, dtype=torch.int64, device=self.device)
+        grouped = self.mode == "group"
+        if grouped:  # segmentation / group rows of cv_group_forward, and the B/m seed scale it writes
+            gwork = torch.zeros(int(_lib.lib().cv_group_workspace_bytes(n, d)) // 4 + 4, dtype=torch.float32,
+                                device=self.device)
+            gscale_rec = torch.ones(1, dtype=torch.float32, device=self.device)
 
         def make_fwd(inject: bool):
             f = Program()
@@ -287,8 +299,16 @@ class ClearStep:
                   (ctypes.c_size_t * len(bufs))(*[nb for _, nb in bufs]), len(bufs))
             pack_program(sp, f, "all")
             ws.encoder_program(f, X, True, zero_heads=False)
-            ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
-            ws.decoder_program(f, ws.z, True, "loss", X)
+            if grouped:
+                hb = ws.heads.data_ptr()
+                f.add("cv_group_forward", self.group_mode, hb, hb + 4 * d, 4 * d, lab, n, d, gwork, gscale_rec,
+                      hb + 8 * d, hb + 12 * d, 4 * d, eps_buf[0] if inject else None, 2 * d, ctypes.c_uint64(self.seed),
+                      None if inject else self.offset, ws.z)
+                ws.decoder_program(f, ws.z, True, "loss", X, rec_scale=gscale_rec)
+                f.keep += [gwork, gscale_rec]
+            else:
+                ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
+                ws.decoder_program(f, ws.z, True, "loss", X)
             # (the running statistics are folded at the end of the backward by cv_step_reduce)
             return f
 
@@ -308,23 +328,32 @@ class ClearStep:
         lat = Program()
         hb = ws.heads.data_ptr()
         dh = ws.dheads.data_ptr()
-        alpha = float(hp["alpha"])
-        tau = float(hp["temperature"])
-        branches = [cv_ntxent_branch(hb, hb + 4 * d, 4 * d, 0, dh, dh + 4 * d, 4 * d, None, alpha,
-                                     ws.losses.data_ptr() + 12, ws.lse[0].data_ptr())]
+        if grouped:
+            lat.add("cv_group_backward", self.group_mode, ws.heads, ws.z, ws.dz, gwork, n, d,
+                    ctypes.c_float(float(hp["beta"])), ctypes.c_float(float(hp.get("loc", 0))),
+                    ctypes.c_float(float(hp.get("scale", 1))), self.anneal, ws.rec, ws.dheads, ws.losses)
+            lat_inj = lat
+            lat.keep.append(gwork)
+            branches = None
+        else:
+            alpha = float(hp["alpha"])
+            tau = float(hp["temperature"])
+            branches = [cv_ntxent_branch(hb, hb + 4 * d, 4 * d, 0, dh, dh + 4 * d, 4 * d, None, alpha,
+                                         ws.losses.data_ptr() + 12, ws.lse[0].data_ptr())]
         if self.mode == "clear":
             ps = bool(hp["ps"])
             branches.append(cv_ntxent_branch(hb + 8 * d, hb + 12 * d, 4 * d, int(ps), dh + 8 * d, dh + 12 * d, 4 * d,
                                              None, alpha if ps else -alpha, ws.losses.data_ptr() + 16,
                                              ws.lse[1].data_ptr()))
-        arr = (cv_ntxent_branch * len(branches))(*branches)
-        # KL + decoder chain into d(heads), then the contrastive terms accumulated on top: two launches
-        lat.add("cv_latent_step", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
-                ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
-                ws.rec, ws.dheads, ws.losses, arr, len(branches), lab, self.sim, ctypes.c_float(tau))
-        lat.keep.append(arr)
-        lat_inj = Program()
-        lat_inj.extend(lat)
+        if branches is not None:
+            arr = (cv_ntxent_branch * len(branches))(*branches)
+            # KL + decoder chain into d(heads) with the contrastive terms accumulated on top
+            lat.add("cv_latent_step", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
+                    ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
+                    ws.rec, ws.dheads, ws.losses, arr, len(branches), lab, self.sim, ctypes.c_float(tau))
+            lat.keep.append(arr)
+            lat_inj = Program()
+            lat_inj.extend(lat)
         if self.mode == "mim":
             mlp = mlp_struct(self.est)
             zp = ws.z.data_ptr()

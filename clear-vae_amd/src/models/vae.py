@@ -112,46 +112,31 @@ class VAE64(VAE):
 
 
 # ----------------------------------------------------------------------------- group evidence
-# GVAE / ML-VAE baselines (reference vae.py:159-223).  Outside the CLEAR hot path (SURVEY 2, row
-# 1b): kept as PyTorch tensor code on the device so the baseline trainers still import and run.
+# GVAE / ML-VAE (reference vae.py:159-223).  The evidence is segmented by label on the device
+# (cvhip.autograd.GroupEvidenceFn -> cv_group_forward / cv_group_evidence_backward); the grouped
+# reparameterisation gathers the group rows into group order, samples them with the HIP sampler (so
+# noise is consumed in the reference's group-after-group order) and scatters back to batch order.
+# The fused trainer step does all of this inside cv_group_forward / cv_group_backward.
 
 
 def accumulate_group_evidence(mu_c, logvar_c, label_batch, mode: str):
-    device = mu_c.device
-    groups = label_batch.unique(sorted=True)
-    mu_acc = torch.zeros(len(groups), mu_c.size(1), device=device)
-    lv_acc = torch.zeros(len(groups), logvar_c.size(1), device=device)
-    group_idx = {}
-    for i, g in enumerate(groups):
-        gl = g.item()
-        sel = label_batch.eq(gl)
-        group_idx[gl] = sel.nonzero().view(-1)
-        if mode == "MLVAE":
-            inv = -logvar_c[sel, :]
-            lse = inv.logsumexp(dim=0)
-            mu_acc[i] = (mu_c[sel, :] * inv.exp()).sum(dim=0) * torch.exp(-lse)
-            lv_acc[i] = -lse
-        elif mode == "GVAE":
-            mu_acc[i] = mu_c[sel, :].mean(dim=0)
-            lv_acc[i] = logvar_c[sel, :].logsumexp(dim=0) - sel.sum().log()
-        else:
-            raise NotImplementedError("only support using MLVAE or GVAE")
-    return mu_acc, lv_acc, group_idx
+    """(mu_g [m, d], logvar_g [m, d], {label: member indices}) (vae.py:159-190)."""
+    _ag._require_gpu(mu_c, logvar_c)
+    meta = {}
+    mu_g, lv_g = _ag.GroupEvidenceFn.apply(mu_c, logvar_c, label_batch, mode, meta)
+    return mu_g, lv_g, meta["groups"]
 
 
 def groupwise_reparam_each(mu_acc_grp, logvar_acc_grp, g_idx: dict):
+    """(z_c [n, d] in batch order, member indices in group order, group size per member) (vae.py:193-223)."""
+    _ag._require_gpu(mu_acc_grp, logvar_acc_grp)
     device = mu_acc_grp.device
-    std = torch.exp(0.5 * logvar_acc_grp)
-    z_grps, indices, sizes = [], [], []
-    for i, (g, idx) in enumerate(g_idx.items()):
-        n = len(idx)
-        eps = torch.randn(n, std.size(1)).to(device)
-        z_grps.append(mu_acc_grp[i][None, :] + eps * std[i][None, :])
-        indices.append(idx)
-        sizes.append(torch.ones_like(idx) * n)
-    z_grps = torch.cat(z_grps, dim=0)
-    indices = torch.cat(indices, dim=0)
-    sizes = torch.cat(sizes, dim=0)
-    inverse = torch.zeros_like(indices)
-    inverse[indices] = torch.arange(len(indices)).to(indices.device)
-    return z_grps[inverse], indices, sizes
+    idx = [i.to(device) for i in g_idx.values()]
+    counts = torch.tensor([len(i) for i in idx], device=device)
+    gid = torch.repeat_interleave(torch.arange(len(idx), device=device), counts)
+    z_sorted = _ag.SampleFn.apply(mu_acc_grp[gid].contiguous(), logvar_acc_grp[gid].contiguous())
+    indices = torch.cat(idx)
+    sizes = counts[gid]
+    inverse = torch.empty_like(indices)
+    inverse[indices] = torch.arange(len(indices), device=device)
+    return z_sorted[inverse], indices, sizes

@@ -11,8 +11,10 @@ replays the reference's loop literally.  Neither path computes on the CPU.
 Per-step scalars that the reference reads with float() every step (trainer.py:486-492, 859, 888)
 are kept on the device and copied once per epoch when the progress bar is disabled.
 ClearTCVAETrainer runs fused too (mode "tc": the factor discriminator's density-ratio
-term and its BCE step as HIP kernels).  The remaining trainers (CNN baselines, downstream probe,
-GVAE/MLVAE) are outside the hot path and keep the reference's PyTorch loops.
+term and its BCE step as HIP kernels), and so does HierarchicalVAETrainer (mode "group":
+the GVAE / ML-VAE group evidence as label-segmented device reductions).  The remaining trainers (CNN
+baselines, downstream probe) are outside the hot path and keep the reference's
+PyTorch loops.
 """
 
 from __future__ import annotations
@@ -432,7 +434,11 @@ class LAMCNNTrainer(SimpleCNNTrainer):
 
 
 class HierarchicalVAETrainer(VAETrainer):
-    """GVAE / ML-VAE baselines (trainer.py:291-412): group-evidence latents, reference loop."""
+    """GVAE / ML-VAE baselines (trainer.py:291-412).  Each step runs as one fused HIP program
+    (cvhip.engine.ClearStep, mode "group"): the group evidence of vae.py:159-223 segmented by label on the
+    device (cv_group_forward / cv_group_backward), kl_c over the groups and the B/m adjustment of rec and
+    kl_s (trainer.py:322-324, 344-349) folded into the backward seed and the latent kernel.  Setups outside
+    the fused contract run the reference's loop on the module-level HIP path."""
 
     def __init__(self, model: VAE, optimizer: Optimizer, hyperparameter: dict[str, float], verbose_period: int,
                  device: torch.device, transform=None) -> None:
@@ -440,6 +446,17 @@ class HierarchicalVAETrainer(VAETrainer):
         self.hyperparameter = hyperparameter
         self.annealer = LogisticAnnealer(loc=hyperparameter["loc"], scale=hyperparameter["scale"],
                                          beta=hyperparameter["beta"])
+        self._engine = None
+        self.use_fused = True
+
+    def _fused(self):
+        if not self.use_fused:
+            return None
+        from cvhip.engine import ClearStep
+
+        if self._engine is None or not self._engine.compatible():
+            self._engine = ClearStep.build(self, mode="group")
+        return self._engine
 
     def fit(self, epochs: int, train_loader: DataLoader, valid_loader: None | DataLoader = None,
             eval_evidence_acc: bool = False):
@@ -455,10 +472,24 @@ class HierarchicalVAETrainer(VAETrainer):
     def _train(self, dataloader: DataLoader, verbose: bool, epoch_id: int):
         vae = self.model
         vae.train()
-        with tqdm(dataloader, unit="batch", disable=not verbose) as bar:
+        engine = self._fused()
+        with tqdm(dataloader, unit="batch", mininterval=0, disable=not verbose) as bar:
             bar.set_description(f"epoch {epoch_id}")
             for batch in bar:
                 X, label = _batch(batch, self.device, None)
+                if engine is not None and engine.accepts(X):
+                    if getattr(self, "_resync", False):
+                        engine.resync_from_host()
+                        self._resync = False
+                    losses = engine.step(X, label)
+                    self.annealer.step()
+                    if verbose:
+                        v = losses.tolist()
+                        bar.set_postfix(reconstr_loss=v[0], kl_c=v[1], kl_s=v[2])
+                    continue
+                if engine is not None:
+                    engine.sync_host_state()
+                    self._resync = True
                 B, m = X.size(0), len(label.unique())
                 if self.transform:
                     X = self.transform(X)
@@ -472,6 +503,8 @@ class HierarchicalVAETrainer(VAETrainer):
                 self.annealer.step()
                 if verbose:
                     bar.set_postfix(reconstr_loss=float(rec), kl_c=float(kl_c), kl_s=float(kl_s))
+        if engine is not None:
+            engine.sync_host_state()
 
     def _valid(self, dataloader, verbose, epoch_id, with_evidence_acc=False):
         if verbose:

@@ -351,6 +351,35 @@ int cv_tc_forward(const cv_tc_disc* D, const float* z, int n, float lam, const f
 int cv_tc_learning_step(const cv_tc_disc* D, const float* z, int n, void* work, float* loss_out,
                         const cv_tc_grad* g, cv_stream_t stream);
 
+/* ---- GVAE / ML-VAE group evidence (vae.py:159-223; HierarchicalVAETrainer, trainer.py:291-353) ----
+ * Segmented by label on the device (n <= 4096, d <= 64): groups in sorted-label order, members in
+ * ascending index (the reference's order).  `work`: cv_group_workspace_bytes(n, d) bytes holding
+ * int32 m at byte 0, then int32 gid[n], pos[n], order[n], start[n+1] at byte 64 onwards and the group rows
+ * mu_g | lv_g [n][2d] fp32 (first m valid) at the next 16-byte boundary. */
+enum { CV_GROUP_MLVAE = 0, CV_GROUP_GVAE = 1 };
+size_t cv_group_workspace_bytes(int n, int d);
+/* accumulate_group_evidence (vae.py:159-190) into `work`; scale_out (or NULL) = n/m, the
+ * _group_adjust factor B/m (trainer.py:322-324).  With z != NULL also groupwise_reparam_each + sample
+ * (vae.py:193-223, 56-60): z [n][2d] = mu_g[gid] + eps_c * exp(lv_g/2) | mu_s + eps_s * exp(lv_s/2), where
+ * row r of the c-noise belongs to the sample at group-order position r (the reference's per-group
+ * torch.randn order).  eps [n][ld_eps] injected (c columns [0,d) in group order, s columns [d,2d) per
+ * sample) or NULL: Philox from (seed, offset[0]), offset[0] += 1. */
+int cv_group_forward(int mode, const float* mu_c, const float* lv_c, int ld, const int64_t* label, int n, int d,
+                     void* work, float* scale_out, const float* mu_s, const float* lv_s, int lds,
+                     const float* eps, int ld_eps, uint64_t seed, uint64_t* offset, float* z, cv_stream_t stream);
+/* The fused step's latent terms (trainer.py:342-349): kl_c over the m group rows, rec and kl_s times
+ * B/m, the annealer weight beta/(1+exp(-(t-loc)/scale)) at t = anneal_step[0], and d(heads) [n][4d]
+ * (written) from dz [n][2d] through the reparameterisation and the evidence.  losses[0..2] = rec
+ * (sum of the CV_REC_REPL rec_in replicas, times B/m), kl_c, kl_s (times B/m); losses[7] = weight. */
+int cv_group_backward(int mode, const float* heads, const float* z, const float* dz, const void* work, int n,
+                      int d, float beta, float loc, float scale, const int64_t* anneal_step,
+                      const double* rec_in, float* dheads, float* losses, cv_stream_t stream);
+/* accumulate_group_evidence backward (module path): d(mu_c), d(lv_c) [n][ldo] (written) from d(mu_g),
+ * d(lv_g) [m][d] (either may be NULL = zero) and the `work` of the matching cv_group_forward. */
+int cv_group_evidence_backward(int mode, const float* mu_c, const float* lv_c, int ld, const void* work, int n,
+                               int d, const float* dmu_g, const float* dlv_g, float* dmu_c, float* dlv_c, int ldo,
+                               cv_stream_t stream);
+
 /* ---- Adam (torch.optim.Adam foreach semantics) over a flat fp32 arena ----
  * hyper: device float[8] = lr, beta1, beta2, eps, weight_decay; step: device int64[2] =
  * (steps taken, arrival counter = 0).  grad_scale (device float or NULL) multiplies the gradient

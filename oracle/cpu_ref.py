@@ -15,6 +15,8 @@ written against torch.nn.functional so that it runs in fp32 or fp64 on the host.
   CLEARVAETrainer step         code/src/trainer.py:447-484
   ClearMIMVAETrainer step      code/src/trainer.py:842-888
   ClearTCVAETrainer step       code/src/trainer.py:648-699
+  GVAE / ML-VAE group evidence code/src/models/vae.py:159-223
+  HierarchicalVAETrainer step  code/src/trainer.py:322-353
 with the reparameterisation noise and the CLUB-S permutation passed in explicitly.
 Gradients come from torch autograd on the CPU.
 
@@ -401,3 +403,73 @@ def tc_factor_loss(D, z):
     dj = disc_forward(D, z)
     dm = disc_forward(D, factor_shuffling(z))
     return F.binary_cross_entropy(torch.cat([dj, dm], dim=0), torch.cat([torch.ones_like(dj), torch.zeros_like(dm)]))
+
+
+# ----------------------------------------------------------------------------- GVAE / ML-VAE
+
+
+def group_evidence(mu_c, lv_c, label, mode):
+    """accumulate_group_evidence (vae.py:159-190).  Groups are the sorted unique labels, members in
+    ascending index.  As in the reference the group rows are held in torch.zeros(...) of the DEFAULT
+    dtype (float32), so they are rounded to fp32 even in an fp64 run."""
+    groups = torch.unique(label, sorted=True)
+    mu_g = torch.zeros(len(groups), mu_c.shape[1])
+    lv_g = torch.zeros(len(groups), lv_c.shape[1])
+    members = {}
+    for i, g in enumerate(groups):
+        sel = label == g
+        members[int(g)] = sel.nonzero().view(-1)
+        if mode == "MLVAE":  # precision-weighted mean, log of the summed precisions
+            lp = -lv_c[sel, :]
+            lse = lp.logsumexp(dim=0)
+            mu_g[i] = (mu_c[sel, :] * lp.exp()).sum(dim=0) * torch.exp(-lse)
+            lv_g[i] = -lse
+        elif mode == "GVAE":  # plain mean, log of the mean variance
+            mu_g[i] = mu_c[sel, :].mean(dim=0)
+            lv_g[i] = lv_c[sel, :].logsumexp(dim=0) - sel.sum().log()
+        else:
+            raise NotImplementedError("only support using MLVAE or GVAE")
+    return mu_g, lv_g, members
+
+
+def group_reparam(mu_g, lv_g, members, eps_sorted):
+    """groupwise_reparam_each (vae.py:193-223) with the noise passed in: row r of eps_sorted belongs to
+    the r-th sample in group order (the reference draws torch.randn(n_g, d) group after group)."""
+    std = torch.exp(0.5 * lv_g)
+    rows, idx, o = [], [], 0
+    for i, (_, ix) in enumerate(members.items()):
+        k = len(ix)
+        rows.append(mu_g[i][None, :] + eps_sorted[o:o + k] * std[i][None, :])
+        idx.append(ix)
+        o += k
+    z_sorted, idx = torch.cat(rows), torch.cat(idx)
+    inverse = torch.zeros_like(idx)
+    inverse[idx] = torch.arange(len(idx))
+    return z_sorted[inverse]
+
+
+def group_order_noise(label, eps_c):
+    """The group-order rows of eps_c (sample-indexed) — the order the reference consumes noise in."""
+    lab = torch.as_tensor(label)
+    order = torch.cat([(lab == g).nonzero().view(-1) for g in torch.unique(lab, sorted=True)])
+    return eps_c[order]
+
+
+def group_step(P, x, label, eps_sorted, eps_s, arch, hp, mode, step=0):
+    """One HierarchicalVAETrainer step's losses and gradients (trainer.py:335-353), no optimizer update:
+    the ELBO on the group rows for kl_c, rec and kl_s times B/m (_group_adjust, :322-324)."""
+    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, True)
+    mu_g, lv_g, members = group_evidence(mu_c, lv_c, label, mode)
+    z = torch.cat([group_reparam(mu_g, lv_g, members, eps_sorted), sample(mu_s, lv_s, eps_s)], dim=-1)
+    xhat = decode(P, z, arch, True)
+    rec, kl_c, kl_s = vae_loss(xhat, x, mu_g, mu_s, lv_g, lv_s)
+    B, m = x.shape[0], len(members)
+    rec_a, kl_s_a = rec * B / m, kl_s * B / m
+    w = anneal_weight(step, hp["beta"], hp.get("loc", 0), hp.get("scale", 1))
+    loss = rec_a + w * kl_c + w * kl_s_a
+    params = {k: v for k, v in P.items() if isinstance(v, torch.Tensor) and v.requires_grad}
+    grads = torch.autograd.grad(loss, list(params.values()), allow_unused=True)
+    return {"xhat": xhat, "z": z, "mu_c": mu_g, "logvar_c": lv_g, "mu_s": mu_s, "logvar_s": lv_s,
+            "mu_c_sample": mu_c, "logvar_c_sample": lv_c, "rec": rec, "kl_c": kl_c, "kl_s": kl_s,
+            "rec_adj": rec_a, "kl_s_adj": kl_s_a, "m": m, "loss": loss,
+            "grads": {k: g for k, g in zip(params, grads)}}

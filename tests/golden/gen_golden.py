@@ -1,13 +1,15 @@
 """Generate the golden fixtures tests/golden/*.npz from the REAL reference (development container only).
 
-Runs one real `CLEARVAETrainer._train` / `ClearMIMVAETrainer._train` / `ClearTCVAETrainer._train` step of
-scotsun/clear-vae
+Runs one real `CLEARVAETrainer._train` / `ClearMIMVAETrainer._train` / `ClearTCVAETrainer._train` /
+`HierarchicalVAETrainer._train` (GVAE / ML-VAE) step of scotsun/clear-vae
 (imported read-only from /root/reference/code, never copied) in float64 on the CPU, with:
   * weights from oracle.cpu_ref.det_state / det_mlp (numpy PCG64, so no weights are stored),
   * inputs from oracle.cpu_ref.det_inputs (seeded; a checksum of them is stored to catch drift),
   * the reparameterisation noise injected through torch.randn_like (vae.py:58, called for c then s
     in VAE.generate, vae.py:70-73) and the CLUB-S permutation through torch.randperm
-    (mi_estimator.py:138), both patched only for the duration of the step,
+    (mi_estimator.py:138), both patched only for the duration of the step; GVAE / ML-VAE draw the content
+    noise group after group with torch.randn(n_g, d) (vae.py:207), which is fed the group-order rows of
+    eps_c (oracle.cpu_ref.group_order_noise),
   * Tensor.cuda neutralised (L1OutUB.forward hardcodes .cuda(), mi_estimator.py:185).
 The losses the trainer computes are captured by wrapping the names src.trainer imported
 (vae_loss, contrastive_loss) and the estimator's forward.  Stored per case: scalars (fp64), the
@@ -55,6 +57,12 @@ CASES = [
     ("vae64_n16_mim_club", "VAE64", 64, 3, 16, 4, "mim", "cosine", None, "CLUBSample", False),
     ("vae_n64_tc", "VAE", 16, 1, 64, 10, "tc", "cosine", None, None, False),
     ("vae64_n16_tc", "VAE64", 64, 3, 16, 4, "tc", "cosine", None, None, False),
+    # GVAE / ML-VAE (the estimator field names the group mode); l40: 32 samples over 40 labels, so
+    # mostly singleton groups and gaps in the label values
+    ("vae_n64_gvae", "VAE", 16, 1, 64, 10, "group", None, None, "GVAE", False),
+    ("vae_n64_mlvae", "VAE", 16, 1, 64, 10, "group", None, None, "MLVAE", True),
+    ("vae_n32_gvae_l40", "VAE", 16, 1, 32, 40, "group", None, None, "GVAE", False),
+    ("vae64_n16_mlvae", "VAE64", 64, 3, 16, 4, "group", None, None, "MLVAE", False),
 ]
 
 HP = {
@@ -132,7 +140,39 @@ def run_case(case):
     out = {}
     try:
         opt = torch.optim.Adam(model.parameters(), lr=hp["lr"])
-        if mode == "clear":
+        if mode == "group":
+            model.mode = est_kind  # VAE(..., group_mode=...) (trainer_utils.py:69-71)
+            L_t = torch.tensor(label)
+            sorted_rows = R.group_order_noise(label, torch.tensor(ec))
+            sizes = [int((L_t == g).sum()) for g in torch.unique(L_t, sorted=True)]
+            chunks = list(torch.split(sorted_rows, sizes))
+            noise.pop(0)  # eps_c is consumed through torch.randn, group by group
+            orig_randn, orig_decode = torch.randn, model.decode
+            zs = []
+
+            def randn(*size, **k):
+                t = chunks.pop(0)
+                assert tuple(t.shape) == tuple(size), (t.shape, size)
+                return t.clone()
+
+            def decode_rec(zz):
+                zs.append(zz.detach().clone())
+                return orig_decode(zz)
+
+            model.decode = decode_rec
+            hyper = {k: hp[k] for k in ("beta", "loc", "scale")}  # get_hierarchical_vae_trainer (:76-80)
+            tr = T.HierarchicalVAETrainer(model, opt, hyper, 1, torch.device("cpu"))
+            torch.randn = randn
+            try:
+                with injected(noise, torch.tensor(perm)):
+                    tr._train([(X, L)], False, 0)
+            finally:
+                torch.randn = orig_randn
+                del model.decode
+            assert not chunks, "unconsumed group noise"
+            out["z"] = zs[0].numpy()
+            out["m"] = np.int64(len(sizes))
+        elif mode == "clear":
             hyper = {k: hp[k] for k in ("temperature", "alpha", "beta", "loc", "scale")}
             hyper["ps"] = ps
             tr = T.CLEARVAETrainer(model, opt, sim_fn, hyper, 1, torch.device("cpu"))
@@ -212,8 +252,9 @@ def run_case(case):
         sys.path.remove(REF)
 
     X_hat, lp, (r_, kc, ks) = rec["vae_loss"][0]
-    out.update(rec=np.float64(r_), kl_c=np.float64(kc), kl_s=np.float64(ks),
-               c_loss=np.float64(rec["contrastive"][0]))
+    out.update(rec=np.float64(r_), kl_c=np.float64(kc), kl_s=np.float64(ks))
+    if mode != "group":
+        out["c_loss"] = np.float64(rec["contrastive"][0])
     if mode == "clear":
         out["s_loss_raw"] = np.float64(rec["contrastive"][1])
         out["s_loss"] = np.float64(rec["contrastive"][1] if ps else -rec["contrastive"][1])
@@ -255,7 +296,7 @@ def main():
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **out)
         print(f"{name}: {os.path.getsize(path) / 1024:.1f} KiB  rec={float(out['rec']):.10g} "
-              f"kl_c={float(out['kl_c']):.10g} c={float(out['c_loss']):.10g}")
+              f"kl_c={float(out['kl_c']):.10g} c={float(out.get('c_loss', np.nan)):.10g}")
 
 
 if __name__ == "__main__":

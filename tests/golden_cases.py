@@ -56,7 +56,11 @@ def oracle_step(fx: dict, dtype=torch.float64) -> dict:
     X, L = torch.tensor(x, dtype=dtype), torch.tensor(label)
     Ec, Es = torch.tensor(ec, dtype=dtype), torch.tensor(es, dtype=dtype)
     out = {}
-    if mode == "clear":
+    if mode == "group":  # GVAE / ML-VAE: the content noise in group order (gen_golden.py)
+        o = R.group_step(P, X, L, R.group_order_noise(label, Ec), Es, arch, hp, m["estimator"])
+        out["z"] = o["z"].detach().numpy()
+        out["m"] = o["m"]
+    elif mode == "clear":
         o = R.clear_step(P, X, L, Ec, Es, arch, hp, m["sim_fn"])
         out["s_loss"] = float(o["s_loss"].detach())
     elif mode == "tc":
@@ -70,7 +74,8 @@ def oracle_step(fx: dict, dtype=torch.float64) -> dict:
         out["mi"] = float(o["mi"].detach())
         out["z"] = o["z"].detach().numpy()
     for k in ("rec", "kl_c", "kl_s", "c_loss"):
-        out[k] = float(o[k].detach())
+        if k in o:
+            out[k] = float(o[k].detach())
     for k in ("mu_c", "logvar_c", "mu_s", "logvar_s"):
         out[k] = o[k].detach().numpy()
     out["xhat"] = o["xhat"].detach().numpy()

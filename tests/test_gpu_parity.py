@@ -49,7 +49,10 @@ def _bias_before_bn(name, arch):
     return R._layer_kind(arch, parts[0], int(parts[1])) in ("conv", "linear")
 
 
-def _check_grads(named_grads, ref_grads, arch):
+def _check_grads(named_grads, ref_grads, arch, floor=(0.0, 0.0)):
+    """floor = (median, global) rel-L2 change of the fp64 reference's own gradients under an fp32-sized
+    input perturbation (_conditioning below): where a step sits on a ReLU knife edge
+    the bars rise to twice that, never below the fixed ones."""
     num, den = 0.0, 0.0
     worst = []
     for k, g_ref in ref_grads.items():
@@ -65,9 +68,28 @@ def _check_grads(named_grads, ref_grads, arch):
         worst.append((_rel(g, g_ref), k))
     worst.sort(reverse=True)
     med = sorted(w for w, _ in worst)[len(worst) // 2]
-    assert med < 5e-4, ("median per-tensor grad rel", med)
-    assert (num / den) ** 0.5 < 2e-3, ("global grad rel", (num / den) ** 0.5, worst[:3])
+    assert med < max(5e-4, 2 * floor[0]), ("median per-tensor grad rel", med, floor)
+    assert (num / den) ** 0.5 < max(2e-3, 2 * floor[1]), ("global grad rel", (num / den) ** 0.5, worst[:3], floor)
     assert worst[0][0] < 2e-2, worst[:3]
+
+
+def _conditioning(ref, step, x, rel=3e-6):
+    """(median per-tensor, global) rel-L2 change of the fp64 oracle's gradients when x moves by `rel`
+    relative — the size of fp32 rounding after a few layers.  The B/m-scaled reconstruction makes the
+    GVAE / ML-VAE gradients decoder-dominated, and some inputs sit on a ReLU knife edge where this is
+    ~1e-3 (VAE n=256 GVAE: 1.8e-3 at 3e-6, 3e-4 already at 1e-7): no fp32 implementation can be held
+    closer than that there."""
+    g = np.random.default_rng(0)
+    o = step(x * (1 + rel * g.standard_normal(x.shape)))
+    rels, num, den = [], 0.0, 0.0
+    for k, b in ref["grads"].items():
+        a = o["grads"][k]
+        if float(b.norm()) < 1e-8:
+            continue
+        rels.append(float((a - b).norm() / b.norm()))
+        num += float((a - b).norm() ** 2)
+        den += float(b.norm() ** 2)
+    return sorted(rels)[len(rels) // 2], (num / den) ** 0.5
 
 
 CASES = [

@@ -23,16 +23,21 @@ def test_fixture_set_complete():
     have = set(G.names())
     for need in ("vae_n64_cosine_ps1", "vae_n64_cosine_ps0", "vae_n64_l2_ps1", "vae_n64_jeffrey_ps1",
                  "vae_n512_cosine_ps1", "vae_n64_mim_club", "vae_n64_mim_l1out", "vae64_n16_cosine_ps1",
-                 "vae64_n16_mim_club", "vae_n64_tc", "vae64_n16_tc"):
+                 "vae64_n16_mim_club", "vae_n64_tc", "vae64_n16_tc", "vae_n64_gvae", "vae_n64_mlvae",
+                 "vae_n32_gvae_l40", "vae64_n16_mlvae"):
         assert need in have, need
 
 
 def test_losses_and_latents(case):
     name, fx, o = case
-    for k in ("rec", "kl_c", "kl_s", "c_loss"):
+    mode = fx["meta"]["mode"]
+    for k in ("rec", "kl_c", "kl_s") + (("c_loss",) if mode != "group" else ()):
         assert abs(o[k] - float(fx[k])) <= TOL * max(abs(float(fx[k])), 1e-3), (name, k, o[k], float(fx[k]))
-    if fx["meta"]["mode"] == "clear":
+    if mode == "clear":
         assert abs(o["s_loss"] - float(fx["s_loss"])) <= TOL * max(abs(float(fx["s_loss"])), 1e-3)
+    elif mode == "group":  # number of groups, and z = grouped reparam | per-sample reparam
+        assert o["m"] == int(fx["m"])
+        assert G.rel(o["z"], fx["z"]) < TOL
     else:
         # the MI term is signed and can be near zero: relative + absolute floor
         assert abs(o["mi"] - float(fx["mi"])) <= TOL * max(abs(float(fx["mi"])), 1.0)
@@ -66,7 +71,7 @@ def test_adam_update_and_buffers(case):
         assert G.rel(ours, ref) < 1e-9 or np.abs(ours - ref).max() <= 1e-4 * lr, (name, k)
     # CLEAR-MIM's 5 extra forwards run on the post-Adam weights, so the running means inherit the
     # noise-level bias steps above (the conv bias shifts the BN input mean one-for-one)
-    btol = 1e-9 if fx["meta"]["mode"] == "clear" else 1e-7  # (CLEAR-TC: one extra forward, as MIM)
+    btol = 1e-9 if fx["meta"]["mode"] in ("clear", "group") else 1e-7  # (CLEAR-TC: one extra forward, as MIM)
     for k, b in o["buffers"].items():
         assert G.rel(b, fx["buf__" + k]) < btol, (name, k)
     if fx["meta"]["mode"] == "mim":
