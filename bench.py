@@ -13,15 +13,18 @@ For N > 1 launch with torch.distributed.run (one process per GPU, RCCL): per-GPU
 
 After the timed region (nothing below is inside it):
   (1) an in-step pass: the step's programs are enqueued eagerly behind a spin kernel long enough for the
-      host to queue the whole step, with a HIP timing-event pair around every call on the stream that call
-      runs on (the main or the weight-gradient side stream), so each call's time is its duration inside a
-      real step, concurrency included; the roofline is priced on the GEMM call with the largest in-step
-      time (`roofline.kernel`), with HBM `traffic` from the committed rocprofv3 PMC passes of that call;
+      host to queue the whole step, with a HIP timing-event pair around every call on the step's stream
+      (single-stream schedule), so each call's time is its duration inside a real step; the roofline is
+      priced on the GEMM call with the largest in-step time (`roofline.kernel`), with HBM `traffic` from
+      the committed rocprofv3 PMC passes of that call;
   (2) on rank 0 at N=1: the CPU baseline (oracle/ref_loop.py, the reference's step composition on
       torch-CPU) on a bounded sample, and the ELBO (and, for CLEAR-MIM, MI) error of one HIP step against
       the fp64 CPU reference on the same batch / weights / noise;
   (3) default config at N=1: configs[2] (CelebA 64x64 bs=256 CLEAR-MIM CLUB-S) is timed the same way
-      and reported under "c3".
+      and reported under "c3";
+  (4) default / camelyon-bf16 config at N=1: the device input pipeline (Resize((64, 64)) + ToTensor of a
+      96x96x3 uint8 batch of 1024, cv_load_batch_u8) under "input_pipeline", with Pillow's own transform
+      timed beside it on one host core.
 """
 
 from __future__ import annotations
@@ -266,7 +269,7 @@ def roofline_of(config, G, instep, precision, engine=None):
     tpath = os.path.join(ROOT, "profiles", f"{config}_traffic.json")
     if os.path.exists(tpath):
         try:
-            t = json.load(open(tpath))["calls"].get(label.split(":")[0])
+            t = json.load(open(tpath))["calls"].get(label)  # full "prog[i]:function" label of this build
             if t is not None:
                 roof["traffic"] = round(float(t["traffic_bytes"]))
         except (OSError, ValueError, KeyError):
@@ -420,6 +423,55 @@ def run_workload(name, cfg, steps, warmup, device, world, rank, detail=True, ker
     return res
 
 
+def pipeline_pass(device, n=1024, hw=96, out=64, reps=50, cpu_budget_s=3.0):
+    """The device input pipeline (cv_load_batch_u8): Resize((64, 64)) + ToTensor of a
+    Camelyon17-shaped batch (96x96x3 uint8 patches resident in HBM, random sample of a 4096-image set;
+    configs[4]'s global batch 1024) timed with HIP events over `reps` back-to-back launches, priced on HBM
+    bytes (uint8 in + fp32 out per image).  Beside it, the reference's own transform — Pillow
+    Image.resize(BILINEAR) + ToTensor's /255, one image at a time on one host core, as its DataLoader
+    (num_workers=0) runs it — on a bounded sample."""
+    import numpy as np
+
+    from cvhip.data import load_batch
+
+    g = np.random.default_rng(0)
+    imgs = torch.tensor(g.integers(0, 256, size=(4096, hw, hw, 3), dtype=np.uint8), device=device)
+    idx = torch.tensor(g.integers(0, 4096, size=n), device=device)
+    dst = torch.empty(n, 3, out, out, dtype=torch.float32, device=device)
+    for _ in range(5):
+        load_batch(imgs, idx, (out, out), out=dst)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        load_batch(imgs, idx, (out, out), out=dst)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000.0 / reps
+    per_img = hw * hw * 3 + 3 * out * out * 4
+    gbs = per_img * n / (us * 1e-6) / 1e9
+    rec = {"op": f"Resize(({out},{out}))+ToTensor of {hw}x{hw}x3 uint8, gather by index (cv_load_batch_u8)",
+           "batch": n, "us_per_batch": round(us, 2), "images_per_s": round(n / (us * 1e-6), 1),
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                        "frac": round(gbs / PEAK_HBM_GBS, 4), "unit": "GB/s", "traffic": None,
+                        "bytes_per_image": per_img}}
+    try:
+        from PIL import Image
+
+        host = imgs[:256].cpu().numpy()
+        t0, k = time.perf_counter(), 0
+        while time.perf_counter() - t0 < cpu_budget_s:
+            im = Image.fromarray(host[k % 256]).resize((out, out), Image.BILINEAR)
+            np.asarray(im, dtype=np.float32).transpose(2, 0, 1) / np.float32(255)
+            k += 1
+        dt = time.perf_counter() - t0
+        rec["cpu_reference"] = {"images_per_s": round(k / dt, 1), "cores": 1, "kind": "reference",
+                                "sample": f"{k} images, Pillow Image.resize(BILINEAR) + /255, {dt:.1f} s"}
+    except ImportError:  # pragma: no cover
+        rec["cpu_reference"] = None
+    return rec
+
+
 def workload_label(name, cfg, world):
     arch, z, C, hw, B, mode, nl, hp, est = cfg
     kind = "CLEAR-VAE" if mode == "clear" else "CLEAR-MIM (CLUB-S)"
@@ -515,6 +567,11 @@ def main():
                 except Exception as e:  # pragma: no cover
                     c3["elbo_rel_err"] = repr(e)
                 rec["c3"] = c3
+            if args.config in ("mnist", "camelyon-bf16") and args.batch is None:
+                try:
+                    rec["input_pipeline"] = pipeline_pass(device)
+                except Exception as e:  # pragma: no cover
+                    rec["input_pipeline"] = {"error": repr(e)}
             if not args.no_cpu_baseline:
                 try:
                     rec["cpu_baseline"] = cpu_baseline(cfg)

@@ -252,6 +252,14 @@ _SIGS = {
         [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
          c_void_p],
     ),
+    "cv_resize_plan_words": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "cv_resize_plan": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_size_t]),
+    "cv_resize_tile_rows": (c_int, [c_void_p, c_int]),
+    "cv_load_batch_u8": (
+        c_int,
+        [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "cv_mi_workspace_bytes": (c_size_t, [c_int]),
     "cv_mi_forward": (
         c_int,

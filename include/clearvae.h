@@ -380,6 +380,27 @@ int cv_group_evidence_backward(int mode, const float* mu_c, const float* lv_c, i
                                int d, const float* dmu_g, const float* dlv_g, float* dmu_c, float* dlv_c, int ldo,
                                cv_stream_t stream);
 
+/* ---- input pipeline (run_pacs_downstream_expr.py:88-98, run_camelyon17_downstream_expr.ipynb cell 6,
+ * data_utils.py:55-73): transforms.Resize((h, w)) + ToTensor() of uint8 images, on the device ----
+ * Resize of a PIL image is Image.resize(size, BILINEAR): Pillow's separable antialiased triangle filter
+ * with 22-bit fixed-point coefficients and an 8-bit intermediate (src/libImaging/Resample.c).  The plan
+ * (int32 words: header, then per output column / row the (first source index, taps) bounds and the
+ * fixed-point coefficients) is built on the host with Pillow's double-precision recipe; copy it to the
+ * device once. */
+size_t cv_resize_plan_words(int in_h, int in_w, int out_h, int out_w);
+int cv_resize_plan(int in_h, int in_w, int out_h, int out_w, int32_t* plan, size_t words);
+/* source rows of the horizontal pass that a tile of `ty` output rows needs (host plan) */
+int cv_resize_tile_rows(const int32_t* plan, int ty);
+/* One batch: out [n][c][out_h][out_w] fp32 = Resize + ToTensor of images[index[i]] (uint8 [count][in_h][in_w][c],
+ * HWC; index NULL = images 0..n-1), identical to Pillow + torchvision bit for bit; labels_out[i] =
+ * labels[index[i]] and styles_out likewise when given.  ty output rows per workgroup, tile_rows =
+ * cv_resize_tile_rows(plan, ty); stage = 1 copies each tile's source rows into LDS first (coalesced).
+ * LDS per workgroup: the plan body + tile_rows * (out_w + stage * in_w) * c bytes, at most 64 KiB. */
+int cv_load_batch_u8(const uint8_t* images, int in_h, int in_w, int c, const int64_t* index, int n,
+                     const int32_t* plan, int out_h, int out_w, int ty, int tile_rows, int stage, float* out,
+                     const int64_t* labels, int64_t* labels_out, const int64_t* styles, int64_t* styles_out,
+                     cv_stream_t stream);
+
 /* ---- Adam (torch.optim.Adam foreach semantics) over a flat fp32 arena ----
  * hyper: device float[8] = lr, beta1, beta2, eps, weight_decay; step: device int64[2] =
  * (steps taken, arrival counter = 0).  grad_scale (device float or NULL) multiplies the gradient

@@ -11,7 +11,11 @@ requests tallied at 64 B), so it is doubled; WRITE_SIZE (KiB) is exact for 16-B 
 atomics.  The per-launch figure is the median over the last --reps dispatches of the call's dominant
 kernel (the warmup steps dispatch the same kernel for other layers first).
 
-    python profiles/pmc_traffic.py <dir> 'enc[4]' <kernel-name-substring> <reps> <out.json>   (merges)
+    python profiles/pmc_traffic.py <dir> 'enc[4]:cv_conv_backward_data' <kernel-name-substring|auto> <reps> <out.json>
+
+(merges into out.json, keyed by the bench's full call label "program[index]:c_function", so a stale entry
+from an older program layout is never matched).  `auto`: the kernel of the trace's last dispatch — in
+--only-call mode the last --reps dispatches are the call's own launches.
 """
 
 import csv
@@ -34,6 +38,15 @@ def per_dispatch(path_glob, counter, kernel_sub):
 
 def main():
     d, call, ksub, reps, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    if ksub == "auto":
+        last = (-1, None)
+        for path in glob.glob(f"{d}/fetch/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(path)):
+                if int(r["Dispatch_Id"]) > last[0]:
+                    last = (int(r["Dispatch_Id"]), r["Kernel_Name"])
+        ksub = last[1]
+        if ksub is None:
+            raise SystemExit(f"no dispatches under {d}")
     fetch = per_dispatch(f"{d}/fetch/**/*counter_collection.csv", "FETCH_SIZE", ksub)[-reps:]
     write = per_dispatch(f"{d}/write/**/*counter_collection.csv", "WRITE_SIZE", ksub)[-reps:]
     if not fetch or not write:

@@ -15,7 +15,7 @@ GOLDEN = os.path.join(HERE, "golden")
 
 
 def names() -> list:
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("resize_"))
 
 
 def load(name: str) -> dict:
