@@ -652,11 +652,28 @@ struct PackArgs {
   float* ds[MAX_PACK];
   int cs[MAX_PACK], cb[MAX_PACK], kk[MAX_PACK];
   int n;
+  // the step's zeroed buffers (cv_pack_conv_weights_zero): the blockIdx.y == n slice clears them
+  uint32_t* zp[8];
+  long zstart[9];  // prefix sums of 4-byte words
+  int zn;
 };
+
+// blockIdx.y == a.n: zero the listed buffers (grid-stride over blockIdx.x)
+__device__ __forceinline__ void pack_zero_slice(const PackArgs& a) {
+  const long total = a.zstart[a.zn];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int b = 0;
+    while (b + 1 < a.zn && i >= a.zstart[b + 1]) ++b;
+    a.zp[b][i - a.zstart[b]] = 0u;
+  }
+}
 // small layers: one destination element per thread, each destination walked in its own order
 __global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
   const int l = blockIdx.y;
-  if (l >= a.n) return;
+  if (l == a.n) {
+    pack_zero_slice(a);
+    return;
+  }
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
   const int total = cs * cbn * kk;
   const float* __restrict__ src = a.src[l];
@@ -680,7 +697,10 @@ constexpr int PK_CS = 16, PK_CB = 32, PK_MAXK = 16;
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   __shared__ float tile[PK_CS * PK_CB * (PK_MAXK + 1)];
   const int l = blockIdx.y;
-  if (l >= a.n) return;
+  if (l == a.n) {
+    pack_zero_slice(a);
+    return;
+  }
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
   const int tcb = (cbn + PK_CB - 1) / PK_CB;
   const int ntile = ((cs + PK_CS - 1) / PK_CS) * tcb;
@@ -1169,11 +1189,19 @@ extern "C" int cv_debug_force_generic_gemm(int on) {
 CV_STAMPS_SETTER(cv_debug_set_stamps)
 #endif
 
-extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream) {
-  clear_error();
+static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, const size_t* zbytes, int zcount,
+                       cv_stream_t stream) {
   CV_REQUIRE(items && n > 0 && n <= MAX_PACK, "pack_conv_weights: 1..%d items", MAX_PACK);
+  CV_REQUIRE(zcount >= 0 && zcount <= 8 && (!zcount || (zptrs && zbytes)), "pack_conv_weights: 0..8 zeroed buffers");
   PackArgs a;
   memset(&a, 0, sizeof(a));
+  a.zn = zcount;
+  for (int i = 0; i < zcount; ++i) {
+    CV_REQUIRE(zptrs[i] && zbytes[i] % 4 == 0 && ((uintptr_t)zptrs[i] & 3) == 0,
+               "pack_conv_weights: zero buffer %d not 4-byte granular", i);
+    a.zp[i] = (uint32_t*)zptrs[i];
+    a.zstart[i + 1] = a.zstart[i] + (long)(zbytes[i] / 4);
+  }
   long mx = 0;
   for (int i = 0; i < n; ++i) {
     const cv_conv_pack& p = items[i];
@@ -1198,11 +1226,27 @@ extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_
     gx = t > gx ? t : gx;
   }
   if (!tiled) gx = (mx + 255) / 256;
+  if (zcount) {
+    const long zg = (a.zstart[zcount] + 255) / 256;
+    gx = zg > gx ? zg : gx;
+  }
   if (gx > 1024) gx = 1024;
-  if (tiled) hipLaunchKernelGGL(pack_kernel, dim3((int)gx, n), dim3(256), 0, S(stream), a);
-  else hipLaunchKernelGGL(pack_small_kernel, dim3((int)gx, n), dim3(256), 0, S(stream), a);
+  const dim3 grid((int)gx, n + (zcount ? 1 : 0));
+  if (tiled) hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, S(stream), a);
+  else hipLaunchKernelGGL(pack_small_kernel, grid, dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("pack_conv_weights");
   return 0;
+}
+
+extern "C" int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream) {
+  clear_error();
+  return pack_launch(items, n, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void* const* zero_ptrs,
+                                         const size_t* zero_bytes, int zero_count, cv_stream_t stream) {
+  clear_error();
+  return pack_launch(items, n, zero_ptrs, zero_bytes, zero_count, stream);
 }
 
 extern "C" int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* bias,

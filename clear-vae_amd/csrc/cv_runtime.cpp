@@ -33,3 +33,56 @@ extern "C" int cv_zero(void* ptr, size_t bytes, cv_stream_t stream) {
   }
   return 0;
 }
+
+// ---- step graphs: capture / replay without a framework in between ----
+// PyTorch's CUDAGraph.replay() refreshes its RNG generators' seed / offset before every launch (two host-to-
+// device copies on the stream, ~5 us each on this runtime); the step graphs use their own device counters, so
+// they are captured and launched directly.
+extern "C" int cv_graph_begin(cv_stream_t stream) {
+  cv::clear_error();
+  hipError_t e = hipStreamBeginCapture(reinterpret_cast<hipStream_t>(stream), hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    cv::set_error("graph_begin: %s", hipGetErrorString(e));
+    return 2;
+  }
+  return 0;
+}
+
+extern "C" int cv_graph_end(cv_stream_t stream, void** exec_out) {
+  cv::clear_error();
+  if (!exec_out) {
+    cv::set_error("graph_end: null exec_out");
+    return 1;
+  }
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(reinterpret_cast<hipStream_t>(stream), &g);
+  if (e != hipSuccess) {
+    cv::set_error("graph_end: capture: %s", hipGetErrorString(e));
+    return 2;
+  }
+  hipGraphExec_t x = nullptr;
+  e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    cv::set_error("graph_end: instantiate: %s", hipGetErrorString(e));
+    return 2;
+  }
+  *exec_out = reinterpret_cast<void*>(x);
+  return 0;
+}
+
+extern "C" int cv_graph_launch(void* exec, cv_stream_t stream) {
+  cv::clear_error();
+  hipError_t e = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) {
+    cv::set_error("graph_launch: %s", hipGetErrorString(e));
+    return 2;
+  }
+  return 0;
+}
+
+extern "C" int cv_graph_destroy(void* exec) {
+  cv::clear_error();
+  if (exec) (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(exec));
+  return 0;
+}

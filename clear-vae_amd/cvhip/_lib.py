@@ -151,6 +151,7 @@ class cv_conv_pack(ctypes.Structure):
 
 _SIGS = {
     "cv_pack_conv_weights": (c_int, [_P(cv_conv_pack), c_int, c_void_p]),
+    "cv_pack_conv_weights_zero": (c_int, [_P(cv_conv_pack), c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "cv_conv_forward": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_data": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_weight": (
@@ -282,6 +283,10 @@ _SIGS = {
     ),
     "cv_bn_param_grads": (c_int, [_P(cv_bn), c_int, _P(c_void_p), _P(c_void_p), c_void_p]),
     "cv_zero": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "cv_graph_begin": (c_int, [c_void_p]),
+    "cv_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "cv_graph_launch": (c_int, [c_void_p, c_void_p]),
+    "cv_graph_destroy": (c_int, [c_void_p]),
     "cv_zero_many": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "cv_copy_many": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "cv_last_error": (ctypes.c_char_p, []),
@@ -341,3 +346,41 @@ def ptr(t) -> int | None:
 
 def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
+
+
+class StepGraph:
+    """An executable HIP graph of library calls, launched without PyTorch's CUDAGraph.replay() (which
+    refreshes the framework's RNG state with two host-to-device copies before every launch)."""
+
+    def __init__(self, record):
+        """record(stream_handle) enqueues the calls; captured on a private stream."""
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        exe = c_void_p()
+        with torch.cuda.stream(side):
+            s = side.cuda_stream
+            call("cv_graph_begin", s)
+            try:
+                record(s)
+            except BaseException:
+                dummy = c_void_p()
+                lib().cv_graph_end(s, ctypes.byref(dummy))
+                if dummy.value:
+                    lib().cv_graph_destroy(dummy)
+                raise
+            call("cv_graph_end", s, ctypes.byref(exe))
+        cur.wait_stream(side)
+        self.exec = exe
+
+    def replay(self, stream=None):
+        call("cv_graph_launch", self.exec, stream_handle() if stream is None else stream)
+
+    def __del__(self):
+        try:
+            if self.exec and self.exec.value:
+                lib().cv_graph_destroy(self.exec)
+                self.exec = None
+        except Exception:  # interpreter shutdown
+            pass
+

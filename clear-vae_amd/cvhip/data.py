@@ -27,6 +27,7 @@ class ResizePlan:
 
     def __init__(self, in_h: int, in_w: int, out_h: int, out_w: int, c: int, device):
         L = _lib.lib()
+        self.out_h = out_h
         words = int(L.cv_resize_plan_words(in_h, in_w, out_h, out_w))
         host = (ctypes.c_int32 * words)()
         _lib.call("cv_resize_plan", in_h, in_w, out_h, out_w, ctypes.addressof(host), words)
@@ -59,15 +60,15 @@ class ResizePlan:
             self.tiles.append((t, rows(t)))
             t //= 2
         self.ty, self.tile_rows = self.tiles[0]
+        self.plan = torch.tensor(list(host), dtype=torch.int32).to(device)
+        self.shape = (in_h, in_w, out_h, out_w, c)
 
     def tile_for(self, n: int):
-        out_h = self.shape[2]
+        out_h = self.out_h
         for ty, tr in self.tiles:
             if n * (-(-out_h // ty)) >= 2048:
                 return ty, tr
         return self.tiles[-1] if len(self.tiles) < 3 else self.tiles[2]
-        self.plan = torch.tensor(list(host), dtype=torch.int32).to(device)
-        self.shape = (in_h, in_w, out_h, out_w, c)
 
     @classmethod
     def get(cls, in_h, in_w, out_h, out_w, c, device):

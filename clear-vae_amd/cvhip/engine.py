@@ -291,13 +291,11 @@ class ClearStep:
 
         def make_fwd(inject: bool):
             f = Program()
-            # one launch zeroes the BN sums, the gradient arena and the two split-K / accumulated
-            # latent buffers of the step
+            # one launch refreshes the packed conv weights and zeroes the BN sums, the gradient arena and the
+            # two split-K / accumulated latent buffers of the step
             bufs = [(ws.stats, ws.stats.numel() * 8), (A.grad, A.numel * 4), (ws.heads, ws.heads.numel() * 4),
                     (ws.dz, ws.dz.numel() * 4)]
-            f.add("cv_zero_many", ptr_array([b.data_ptr() for b, _ in bufs]),
-                  (ctypes.c_size_t * len(bufs))(*[nb for _, nb in bufs]), len(bufs))
-            pack_program(sp, f, "all")
+            pack_program(sp, f, "all", zero=bufs)
             ws.encoder_program(f, X, True, zero_heads=False)
             if grouped:
                 hb = ws.heads.data_ptr()
@@ -522,16 +520,18 @@ class ClearStep:
         return True
 
     def _capture(self, G):
+        """One executable HIP graph per program segment (_lib.StepGraph: launched directly, without
+        PyTorch's per-replay RNG bookkeeping)."""
         graphs = []
         for item in self._segments(G, False):
             if item[0] != "prog":
                 continue
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                s = _lib.stream_handle()
-                for P in item[1]:
+
+            def record(s, progs=item[1]):
+                for P in progs:
                     P.run(s)
-            graphs.append(g)
+
+            graphs.append(_lib.StepGraph(record))
         G["graphs"] = graphs
 
     # ----------------------------------------------------------------------------- one step

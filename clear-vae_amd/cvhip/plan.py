@@ -289,11 +289,19 @@ def attach_packed(spec: VaeSpec, device):
     spec.packed = buf
 
 
-def pack_program(spec: VaeSpec, P: "Program", which: str = "all"):
-    """Refresh the packed conv weights from the (arena) parameters: one launch."""
+def pack_program(spec: VaeSpec, P: "Program", which: str = "all", zero=None):
+    """Refresh the packed conv weights from the (arena) parameters: one launch; `zero` = [(tensor,
+    bytes)] buffers cleared by the same launch."""
     items = spec.pack_items["enc"] * (which != "dec") + spec.pack_items["dec"] * (which != "enc")
-    if items:
+    if items and zero:
+        P.add("cv_pack_conv_weights_zero", struct_array(cv_conv_pack, items), len(items),
+              ptr_array([t.data_ptr() for t, _ in zero]), (ctypes.c_size_t * len(zero))(*[nb for _, nb in zero]),
+              len(zero))
+    elif items:
         P.add("cv_pack_conv_weights", struct_array(cv_conv_pack, items), len(items))
+    elif zero:
+        P.add("cv_zero_many", ptr_array([t.data_ptr() for t, _ in zero]),
+              (ctypes.c_size_t * len(zero))(*[nb for _, nb in zero]), len(zero))
 
 
 # ----------------------------------------------------------------------------- BN plumbing

@@ -122,6 +122,10 @@ typedef struct cv_conv_pack {
   int cs, cb, kh, kw;
 } cv_conv_pack;
 int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream);
+/* cv_pack_conv_weights plus, in the same launch, zeroing of up to 8 buffers (4-byte granular) that are not
+ * touched by the packing: the first launch of a training step clears the step's accumulators with it. */
+int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void* const* zero_ptrs, const size_t* zero_bytes,
+                              int zero_count, cv_stream_t stream);
 
 /* y = conv(T(x)) + bias.  Replaces nn.Conv2d/ConvTranspose2d.forward (vae.py:15-46) with the
  * preceding BatchNorm2d+ReLU fused into the operand load and the following BatchNorm2d's batch
@@ -430,6 +434,13 @@ int cv_zero(void* ptr, size_t bytes, cv_stream_t stream);
 int cv_zero_many(void* const* ptrs, const size_t* bytes, int count, cv_stream_t stream);
 /* device-to-device copy of up to 8 buffers (4-byte granular) in one launch (the step's input batch) */
 int cv_copy_many(void* const* dst, const void* const* src, const size_t* bytes, int count, cv_stream_t stream);
+/* Step graphs: capture the calls enqueued on `stream` between cv_graph_begin and cv_graph_end (thread-local
+ * capture mode; the stream must not be the legacy default stream) into an executable graph, replay it with
+ * cv_graph_launch on any stream, free it with cv_graph_destroy. */
+int cv_graph_begin(cv_stream_t stream);
+int cv_graph_end(cv_stream_t stream, void** exec_out);
+int cv_graph_launch(void* exec, cv_stream_t stream);
+int cv_graph_destroy(void* exec);
 const char* cv_last_error(void);
 int cv_version(void);
 /* test hook: 1 routes every conv/linear GEMM to the generic implicit-GEMM kernel instead of the

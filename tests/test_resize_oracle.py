@@ -108,3 +108,18 @@ def test_kernel_tiling_emulation(fixture, case, ty):
     got = _emulate(img, P, oh, ow, ty)
     ref = fixture[name + "__out"][0].transpose(2, 0, 1).astype(np.float32) / np.float32(255)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("sz", SIZES, ids=["x".join(map(str, s)) for s in SIZES])
+def test_resize_plan_tiles(sz):
+    """cvhip.data.ResizePlan (host side): tiles fit the LDS budget, small batches get shorter tiles."""
+    from cvhip.data import ResizePlan
+
+    in_h, in_w, out_h, out_w = sz
+    p = ResizePlan(in_h, in_w, out_h, out_w, 3, "cpu")
+    words = p.plan.numel()
+    for ty, tr in p.tiles:
+        assert 4 * (words - 16) + 16 + tr * (out_w + (in_w if p.stage else 0)) * 3 <= 64 * 1024
+    ty_big, _ = p.tile_for(4096)
+    ty_small, _ = p.tile_for(8)
+    assert ty_big >= ty_small
