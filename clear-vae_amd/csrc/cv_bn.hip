@@ -463,6 +463,8 @@ __global__ __launch_bounds__(256) void declinear_wgrad_kernel(int n, int F, int 
 // BatchNorm affine gradients from the backward sums, and the running statistics from the forward sums.
 // Replaces one wgrad_reduce launch per weight gradient, cv_bn_param_grads (x2) and cv_bn_update_running.
 constexpr int MAX_DEFER = 24;
+constexpr int MAX_PLAIN = 32;
+constexpr int SR_PLAIN = 1024;  // arena elements per Adam block of the plain ranges
 struct StepRedArgs {
   cv_wgrad_defer d[MAX_DEFER];
   int blk0[MAX_DEFER + 1];  // prefix sums of the reduction blocks of each deferred gradient
@@ -473,15 +475,58 @@ struct StepRedArgs {
   int64_t* nbt[MAX_BN];
   int nbn, grads, running;
   float momentum;
+  // fused Adam (cv_step_reduce_adam; ap == nullptr: off).  Every gradient this launch finalises is stepped
+  // where it is produced; the rest of the arena lies in the plain ranges [plain0, plain0 + plainn), stepped
+  // by the trailing blocks (pblk0: prefix sums of their blocks)
+  float* ap;
+  float* ag;
+  float* am;
+  float* av;
+  const float* hyper;
+  int64_t* step;
+  int64_t* aux;
+  long plain0[MAX_PLAIN];
+  int plainn[MAX_PLAIN];
+  int pblk0[MAX_PLAIN + 1];
+  int nplain;
+  int nprod;  // blocks that reduce the deferred segments (grid-stride over blk0[nd] segments)
 };
 constexpr int SR_E = 64;           // partial-tile elements per block: 256-byte row segments
 constexpr int SR_G = 256 / SR_E;   // split groups per element (each thread sums every SR_G-th split)
 
-__global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
-  __shared__ float red[SR_G][SR_E + 1];
-  __shared__ double scratch[4 * 256];
-  const int b = blockIdx.x, t = threadIdx.x;
-  if (b < a.blk0[a.nd]) {
+// torch.optim.Adam (foreach) on one element of the arena, constants from adam_consts
+struct AdamC {
+  float step_size, bc2s, omb1, omb2, b2, eps, wd;
+};
+__device__ __forceinline__ AdamC adam_consts(const float* hyper, int64_t step0) {
+  const long t_step = step0 + 1;
+  const double b1 = hyper[1], b2 = hyper[2];
+  const double bc1 = 1.0 - pow(b1, (double)t_step);
+  const double bc2 = 1.0 - pow(b2, (double)t_step);
+  AdamC c;
+  c.step_size = (float)(-(double)hyper[0] / bc1);
+  c.bc2s = (float)sqrt(bc2);
+  c.omb1 = (float)(1.0 - b1);
+  c.omb2 = (float)(1.0 - b2);
+  c.b2 = hyper[2];
+  c.eps = hyper[3];
+  c.wd = hyper[4];
+  return c;
+}
+__device__ __forceinline__ void adam_elem(const StepRedArgs& a, const AdamC& c, long i, float g) {
+  float pp = a.ap[i], mm = a.am[i], vv = a.av[i];
+  if (c.wd != 0.f) g = g + c.wd * pp;
+  mm = mm + c.omb1 * (g - mm);
+  vv = vv * c.b2 + c.omb2 * g * g;
+  const float den = sqrtf(vv) / c.bc2s + c.eps;
+  a.ap[i] = pp + c.step_size * (mm / den);
+  a.am[i] = mm;
+  a.av[i] = vv;
+}
+
+__device__ __forceinline__ void defer_segment(const StepRedArgs& a, const AdamC& ac, bool adam, int b, int t,
+                                              float (*red)[SR_E + 1]) {
+  {
     int di = 0;
     while (di + 1 < a.nd && b >= a.blk0[di + 1]) ++di;
     const cv_wgrad_defer& d = a.d[di];
@@ -508,17 +553,40 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
 #pragma unroll
       for (int g = 0; g < SR_G; ++g) v += red[g][t];  // fixed order: deterministic
       const int row = (int)(o / d.ntot), col = (int)(o - (long)row * d.ntot);
+      float* dst = nullptr;
       if (col < d.N) {
         const int tap = col / d.cb, c = col - tap * d.cb;
-        d.gweight[((size_t)row * d.cb + c) * d.kk + tap] += v;
+        dst = d.gweight + ((size_t)row * d.cb + c) * d.kk + tap;
       } else if (d.gbias) {
-        d.gbias[row] += v;
+        dst = d.gbias + row;
+      }
+      if (dst) {
+        const float g = *dst + v;
+        *dst = g;
+        if (adam) adam_elem(a, ac, dst - a.ag, g);
       }
     }
+    __syncthreads();  // (red is reused by the block's next segment)
+  }
+}
+
+__device__ __forceinline__ void step_reduce_body(const StepRedArgs& a, const AdamC& ac, bool adam, int b, int t,
+                                                 float (*red)[SR_E + 1], double* scratch) {
+  if (b < a.nprod) {  // deferred weight gradients: segments of 64 partial-tile elements, grid-stride
+    for (int sgm = b; sgm < a.blk0[a.nd]; sgm += a.nprod) defer_segment(a, ac, adam, sgm, t, red);
     return;
   }
-  const int l = b - a.blk0[a.nd];
-  if (l >= a.nbn) return;
+  const int l = b - a.nprod;
+  if (l >= a.nbn) {  // fused Adam over a plain range of the arena
+    const int pb = l - a.nbn;
+    if (!adam || pb >= a.pblk0[a.nplain]) return;
+    int r = 0;
+    while (r + 1 < a.nplain && pb >= a.pblk0[r + 1]) ++r;
+    const long i0 = a.plain0[r] + (long)(pb - a.pblk0[r]) * SR_PLAIN;
+    const long i1 = min(a.plain0[r] + (long)a.plainn[r], i0 + SR_PLAIN);
+    for (long i = i0 + t; i < i1; i += 256) adam_elem(a, ac, i, a.ag[i]);
+    return;
+  }
   const cv_bn& bn = a.bn[l];
   if (a.grads) {  // dgamma = sum dz*xhat, dbeta = sum dz (the backward sums)
     cv_bn gb = bn;
@@ -526,8 +594,14 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
     float* dg = a.dg[l];
     float* db = a.db[l];
     bn_fold<256>(gb, false, scratch, [&](int c, double s1, double s2, double, double) {
-      if (db) db[c] = (float)s1;
-      if (dg) dg[c] = (float)s2;
+      if (db) {
+        db[c] = (float)s1;
+        if (adam) adam_elem(a, ac, db + c - a.ag, (float)s1);
+      }
+      if (dg) {
+        dg[c] = (float)s2;
+        if (adam) adam_elem(a, ac, dg + c - a.ag, (float)s2);
+      }
     });
   }
   if (a.running) {  // running statistics, momentum update with the unbiased batch variance
@@ -544,6 +618,40 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
       rm[c] = m * (float)mean + (1.0f - m) * rm[c];
       rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
     });
+  }
+}
+
+__global__ __launch_bounds__(256) void step_reduce_kernel(const StepRedArgs a) {
+  __shared__ float red[SR_G][SR_E + 1];
+  __shared__ double scratch[4 * 256];
+  __shared__ AdamC acs;
+  __shared__ int last;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const bool adam = a.ap != nullptr;
+  if (adam) {
+    if (t == 0) acs = adam_consts(a.hyper, a.step[0]);  // every block reads step[0] before its ticket
+    __syncthreads();
+  }
+  const AdamC ac = adam ? acs : AdamC{};
+  step_reduce_body(a, ac, adam, b, t, red, scratch);
+  if (adam) {  // the last block to arrive advances the step (and annealer) counters: arrivals counted in two
+    __syncthreads();  // levels (64 group words step[2..65], then step[1]) so blocks do not serialise on one word
+    if (t == 0) {
+      const unsigned nblk = gridDim.x, gsz = (nblk + 63) / 64, ngrp = (nblk + gsz - 1) / gsz, grp = b / gsz;
+      const unsigned gcnt = (grp + 1 == ngrp) ? nblk - grp * gsz : gsz;
+      unsigned long long* gw = reinterpret_cast<unsigned long long*>(a.step + 2 + grp);
+      last = 0;
+      if (atomicAdd(gw, 1ull) == gcnt - 1) {
+        *gw = 0;
+        last = atomicAdd((unsigned long long*)(a.step + 1), 1ull) == ngrp - 1;
+      }
+    }
+    __syncthreads();
+    if (last && t == 0) {
+      a.step[0] += 1;
+      a.step[1] = 0;
+      if (a.aux) a.aux[0] += 1;
+    }
   }
 }
 
@@ -763,10 +871,35 @@ extern "C" int cv_declinear_backward_weight(const cv_linear* g, float* da, const
   return 0;
 }
 
+static int step_reduce_launch(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn,
+                              float* const* dgamma, float* const* dbeta, int running, float momentum,
+                              int64_t* const* nbt, const float* adam_arena[4], int64_t numel, const float* hyper,
+                              int64_t* step, int64_t* aux, cv_stream_t stream);
+
 extern "C" int cv_step_reduce(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn, float* const* dgamma,
                               float* const* dbeta, int running, float momentum, int64_t* const* nbt,
                               cv_stream_t stream) {
   clear_error();
+  return step_reduce_launch(defers, ndefer, bn, nbn, dgamma, dbeta, running, momentum, nbt, nullptr, 0, nullptr,
+                            nullptr, nullptr, stream);
+}
+
+extern "C" int cv_step_reduce_adam(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn,
+                                   float* const* dgamma, float* const* dbeta, int running, float momentum,
+                                   int64_t* const* nbt, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                                   int64_t numel, const float* hyper, int64_t* step, int64_t* aux_counter,
+                                   cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(params && grads && exp_avg && exp_avg_sq && hyper && step && numel > 0, "step_reduce_adam: bad arena");
+  const float* arena[4] = {params, grads, exp_avg, exp_avg_sq};
+  return step_reduce_launch(defers, ndefer, bn, nbn, dgamma, dbeta, running, momentum, nbt, arena, numel, hyper,
+                            step, aux_counter, stream);
+}
+
+static int step_reduce_launch(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn,
+                              float* const* dgamma, float* const* dbeta, int running, float momentum,
+                              int64_t* const* nbt, const float* adam_arena[4], int64_t numel, const float* hyper,
+                              int64_t* step, int64_t* aux, cv_stream_t stream) {
   CV_REQUIRE(ndefer >= 0 && ndefer <= MAX_DEFER && nbn >= 0 && nbn <= MAX_BN, "step_reduce: <= %d gradients, <= %d BN layers",
              MAX_DEFER, MAX_BN);
   CV_REQUIRE(ndefer == 0 || defers, "step_reduce: null defer list");
@@ -799,7 +932,69 @@ extern "C" int cv_step_reduce(const cv_wgrad_defer* defers, int ndefer, const cv
   a.grads = (dgamma || dbeta) ? 1 : 0;
   a.running = running;
   a.momentum = momentum;
-  const int blocks = nb + nbn;
+  // without Adam every segment has its own block (no arrival ticket); with it the segments are shared by at most
+  // 2048 blocks so the ticket stays cheap
+  a.nprod = adam_arena ? (nb < 2048 ? nb : 2048) : nb;
+  int blocks = a.nprod + nbn;
+  if (adam_arena) {
+    // the gradient ranges this launch finalises (steps them itself); the complement is stepped by plain blocks
+    const float* g0 = adam_arena[1];
+    struct Iv { long lo, hi; };
+    Iv iv[3 * MAX_DEFER + 2 * MAX_BN];
+    int niv = 0;
+    auto cover = [&](const float* p, long n) -> int {
+      if (!p || n <= 0) return 0;
+      const long lo = (long)(p - g0);
+      CV_REQUIRE(lo >= 0 && lo + n <= numel, "step_reduce_adam: a reduced gradient lies outside the arena");
+      iv[niv++] = {lo, lo + n};
+      return 0;
+    };
+    for (int i = 0; i < a.nd; ++i) {
+      const cv_wgrad_defer& d = a.d[i];
+      if (cover(d.gweight, (long)d.M * d.cb * d.kk)) return 1;
+      if (d.ntot > d.N && cover(d.gbias, d.M)) return 1;
+    }
+    for (int i = 0; i < nbn; ++i) {
+      if (a.grads && cover(a.dg[i], a.bn[i].C)) return 1;
+      if (a.grads && cover(a.db[i], a.bn[i].C)) return 1;
+    }
+    for (int i = 1; i < niv; ++i)  // insertion sort by start
+      for (int j = i; j > 0 && iv[j].lo < iv[j - 1].lo; --j) {
+        const Iv tmp = iv[j];
+        iv[j] = iv[j - 1];
+        iv[j - 1] = tmp;
+      }
+    long pos = 0;
+    int pb = 0;
+    auto plain = [&](long lo, long hi) -> int {
+      while (lo < hi) {
+        CV_REQUIRE(a.nplain < MAX_PLAIN, "step_reduce_adam: more than %d plain ranges", MAX_PLAIN);
+        const long n = hi - lo < (1L << 30) ? hi - lo : (1L << 30);
+        a.plain0[a.nplain] = lo;
+        a.plainn[a.nplain] = (int)n;
+        a.pblk0[a.nplain] = pb;
+        pb += (int)((n + SR_PLAIN - 1) / SR_PLAIN);
+        ++a.nplain;
+        lo += n;
+      }
+      return 0;
+    };
+    for (int i = 0; i < niv; ++i) {
+      CV_REQUIRE(iv[i].lo >= pos, "step_reduce_adam: overlapping reduced gradients");
+      if (plain(pos, iv[i].lo)) return 1;
+      pos = iv[i].hi;
+    }
+    if (plain(pos, numel)) return 1;
+    a.pblk0[a.nplain] = pb;
+    a.ap = const_cast<float*>(adam_arena[0]);
+    a.ag = const_cast<float*>(adam_arena[1]);
+    a.am = const_cast<float*>(adam_arena[2]);
+    a.av = const_cast<float*>(adam_arena[3]);
+    a.hyper = hyper;
+    a.step = step;
+    a.aux = aux;
+    blocks += pb;
+  }
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(step_reduce_kernel, dim3(blocks), dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("step_reduce");

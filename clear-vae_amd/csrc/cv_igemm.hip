@@ -1071,7 +1071,13 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k) {
   if (split_k > 0) {
     split = split_k;
   } else {
-    split = (1024 + tiles - 1) / tiles;
+    static long target = -1;  // A/B override: CV_WGRAD_TARGET (workgroups the split aims for)
+    if (target < 0) {
+      const char* e = getenv("CV_WGRAD_TARGET");
+      target = e ? atol(e) : 1024;
+      if (target < 1) target = 1024;
+    }
+    split = (target + tiles - 1) / tiles;
     long maxs = ktiles / 8;
     if (tiles * maxs < 256) maxs = ktiles / 4;
     if (maxs < 1) maxs = 1;

@@ -173,6 +173,11 @@ _SIGS = {
         [_P(cv_wgrad_defer), c_int, _P(cv_bn), c_int, _P(c_void_p), _P(c_void_p), c_int, c_float, _P(c_void_p),
          c_void_p],
     ),
+    "cv_step_reduce_adam": (
+        c_int,
+        [_P(cv_wgrad_defer), c_int, _P(cv_bn), c_int, _P(c_void_p), _P(c_void_p), c_int, c_float, _P(c_void_p),
+         c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "cv_conv_wgrad_workspace_bytes": (c_size_t, [_P(cv_conv), c_int]),
     "cv_linear_wgrad_workspace_bytes": (c_size_t, [_P(cv_linear), c_int]),
     "cv_linear_forward": (

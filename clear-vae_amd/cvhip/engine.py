@@ -35,6 +35,7 @@ between its gradient and Adam segments.  Semantics are those of torch DDP around
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -44,6 +45,12 @@ from . import dist as cvdist
 from ._lib import GROUP, MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch, cv_tc_disc, cv_tc_grad
 from .autograd import est_params, mlp_struct
 from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
+
+
+# CVHIP_FUSED_ADAM=1: single-process steps run the optimizer inside the end-of-backward reduction
+# (cv_step_reduce_adam: one launch less, but the reduction's gradient order makes the Adam read-modify-writes
+# strided; MNIST 777k vs 791k img/s, CelebA 99.7k vs 102.3k), so the separate cv_adam_step stays the default
+FUSED_ADAM = os.environ.get("CVHIP_FUSED_ADAM", "0") == "1"  # measured slower (strided Adam RMW): off
 
 
 def disc_params(disc):
@@ -89,7 +96,9 @@ class _AdamState:
                     self.v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
                     steps = int(float(st["step"]))
         self.host_steps = steps
-        self.step = torch.tensor([steps, 0], dtype=torch.int64, device=dev)
+        # [steps taken, arrival word, 64 group arrival words (cv_step_reduce_adam)]
+        self.step = torch.zeros(2 + 64, dtype=torch.int64, device=dev)
+        self.step[0] = steps
         self.hyper_host = None
         self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
         self.refresh_hyper()
@@ -372,11 +381,18 @@ class ClearStep:
         if dp:  # encoder bucket: its gradients and BN affine grads; every layer's running statistics
             ws.step_reduce_program(enc, enc_defer, pg, "enc", running=False)
             ws.running_program(enc, "all")
-        else:
-            ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
         upd = Program()
-        upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper, self.adam.step,
-                self.gscale if self.world > 1 else None, self.anneal)
+        if dp:
+            upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
+                    self.adam.step, self.gscale, self.anneal)
+        elif not FUSED_ADAM:
+            ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
+            upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
+                    self.adam.step, None, self.anneal)
+        else:  # single process: the optimizer step rides in the end-of-backward reduction launch
+            ws.step_reduce_program(enc, enc_defer, pg, "all", running=True,
+                                   adam=(A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
+                                         self.adam.step, self.anneal))
         learn = learn_inj = None
         if self.mode == "mim":
             E = self.est_arena

@@ -610,14 +610,20 @@ class Workspace:
         P.add(name, geom, a, b, gw, gb, buf, buf.numel() * 4, defer.next())
 
     def step_reduce_program(self, P: "Program", defer: "DeferGroup", param_grad, which: str = "all",
-                            running: bool = True):
+                            running: bool = True, adam=None):
         """cv_step_reduce: the group's deferred weight gradients, the BN affine gradients of `which`
-        layers and (running=True) their running statistics, in one launch."""
+        layers and (running=True) their running statistics, in one launch.  adam = (params, grads, exp_avg,
+        exp_avg_sq, numel, hyper, step, aux_counter): cv_step_reduce_adam, the optimizer step in the same
+        launch."""
         views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
         bns = struct_array(cv_bn, [b.cv(True) for b in views])
         dg = ptr_array([param_grad(b.mod.weight) for b in views])
         db = ptr_array([param_grad(b.mod.bias) for b in views])
         nbt = ptr_array([b.mod.num_batches_tracked.data_ptr() for b in views]) if running else None
+        if adam is not None:
+            P.add("cv_step_reduce_adam", defer.arr, defer.n, bns, len(views), dg, db, int(running),
+                  ctypes.c_float(float(views[0].mod.momentum)), nbt, *adam)
+            return
         P.add("cv_step_reduce", defer.arr, defer.n, bns, len(views), dg, db, int(running),
               ctypes.c_float(float(views[0].mod.momentum)), nbt)
 

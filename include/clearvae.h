@@ -422,6 +422,17 @@ int cv_adam_step(float* params, const float* grads, float* exp_avg, float* exp_a
 int cv_step_reduce(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn, float* const* dgamma,
                    float* const* dbeta, int running, float momentum, int64_t* const* nbt, cv_stream_t stream);
 
+/* cv_step_reduce + cv_adam_step (no grad_scale) in the same launch, for a single-process step: every
+ * gradient the reduction finalises (deferred weights / biases, dgamma, dbeta — all inside the gradient arena
+ * grads[0, numel)) is stepped as soon as it is produced, the rest of the arena (its gradients already final) by
+ * trailing blocks; the last block advances step[0] and aux_counter.  step: device int64[66] = (steps taken, then
+ * 65 zeroed arrival words, which reset themselves).  The reduced ranges must not overlap and, with the gaps
+ * between them, form at most 32 plain ranges. */
+int cv_step_reduce_adam(const cv_wgrad_defer* defers, int ndefer, const cv_bn* bn, int nbn, float* const* dgamma,
+                        float* const* dbeta, int running, float momentum, int64_t* const* nbt, float* params,
+                        float* grads, float* exp_avg, float* exp_avg_sq, int64_t numel, const float* hyper,
+                        int64_t* step, int64_t* aux_counter, cv_stream_t stream);
+
 /* BatchNorm affine gradients from the backward sums: dgamma = sum dz*xhat, dbeta = sum dz
  * (nn.BatchNorm weight/bias grads); written (not accumulated) for up to 16 layers. */
 int cv_bn_param_grads(const cv_bn* bn, int nlayers, float* const* dgamma, float* const* dbeta,
