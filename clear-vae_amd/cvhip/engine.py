@@ -400,13 +400,25 @@ class ClearStep:
             G = cv_mlp_grad(*[E.gptr(p) for p in est_params(self.est)])
             zp = ws.z.data_ptr()
 
+            # The 5 estimator updates (trainer.py:873-888) each run a train-mode forward of the same batch through
+            # the same (post-Adam) VAE: the encoder, its batch statistics and the heads are identical in all five,
+            # so they are computed once; each update re-runs the reparameterisation (fresh noise), the decoder
+            # (its statistics follow z) and the running-statistics update of every layer (the encoder's five
+            # momentum updates with its one set of batch statistics, as in five forwards)
+            def learn_forward(prog, j, inject):
+                if j == 0:
+                    prog.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+                    ws.encoder_program(prog, X, True)
+                else:
+                    prog.add("cv_zero_many", ptr_array([ws.dec_stats.data_ptr(), ws.dec_tickets.data_ptr()]),
+                             (ctypes.c_size_t * 2)(ws.dec_stats.numel() * 8, ws.dec_tickets.numel() * 8), 2)
+                ws.reparam_program(prog, eps_buf[1 + j] if inject else None, self.seed, self.offset)
+
             def make_learn(inject: bool):
                 lp = Program()
                 pack_program(sp, lp, "all")  # the VAE Adam step just moved the weights
                 for j in range(5):
-                    lp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-                    ws.encoder_program(lp, X, True)
-                    ws.reparam_program(lp, eps_buf[1 + j] if inject else None, self.seed, self.offset)
+                    learn_forward(lp, j, inject)
                     ws.decoder_program(lp, ws.z, True, "none")
                     ws.running_program(lp, "all")
                     lp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
@@ -422,9 +434,7 @@ class ClearStep:
                     gp = Program()
                     if j == 0:
                         pack_program(sp, gp, "all")
-                    gp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-                    ws.encoder_program(gp, X, True)
-                    ws.reparam_program(gp, eps_buf[1 + j] if inject else None, self.seed, self.offset)
+                    learn_forward(gp, j, inject)
                     ws.decoder_program(gp, ws.z, True, "none")
                     ws.running_program(gp, "all")
                     gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,

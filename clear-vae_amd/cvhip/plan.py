@@ -571,6 +571,12 @@ class Workspace:
             bv.fin_fwd = j + 1 < nd and bv.C % 32 == 0  # (layer nd-2: read by the edge scatter / wgrad)
             bv.fin_bwd = j + 2 < nd and bv.C % 32 == 0
         self.rec = self.scal[0:_lib.REC_REPL]
+        # the decoder layers' statistics and arrival tickets (contiguous: BatchNorm1d then the ConvT layers), for
+        # forwards that reuse the encoder of the previous one (CLEAR-MIM's estimator updates)
+        ne = len(spec.enc)
+        d0 = sum(2 * _lib.stat_repl(b.num_features) * 2 * b.num_features for b in bns[:ne])
+        self.dec_stats = self.stats[d0:o]
+        self.dec_tickets = self.stats[o + 64 + tw * ne:o + 64 + tw * len(bns)]
         if with_grad:
             self.g_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]
             self.dheads = torch.empty(n, 4 * d, **f32)
