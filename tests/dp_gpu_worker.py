@@ -37,13 +37,13 @@ def run(rank, world, port, q, mode, n_global, kind):
         from oracle import cpu_ref as R
         from src.models.mi_estimator import CLUBSample, L1OutUB
         from src.models.vae import VAE
-        from src.trainer import ClearMIMVAETrainer, CLEARVAETrainer
+        from src.trainer import ClearMIMVAETrainer, ClearTCVAETrainer, CLEARVAETrainer, HierarchicalVAETrainer
 
         zt, C = 16, 1
         sd = R.det_state("VAE", zt, C)
         if rank != 0:  # a different start on rank 1: the engine must adopt rank 0's weights
             sd = {k: (v * 1.25 if np.asarray(v).dtype != np.int64 else v) for k, v in sd.items()}
-        vae = VAE(zt, C).cuda()
+        vae = VAE(zt, C, group_mode=kind if mode == "group" else None).cuda()
         vae.load_state_dict({k: torch.as_tensor(np.asarray(v)).float() if np.asarray(v).dtype != np.int64
                              else torch.as_tensor(np.asarray(v)) for k, v in sd.items()})
         opt = torch.optim.Adam(vae.parameters(), lr=5e-4)
@@ -51,6 +51,18 @@ def run(rank, world, port, q, mode, n_global, kind):
         if mode == "clear":
             hp = {"temperature": 0.1, "alpha": 100.0, "beta": 0.125, "ps": True, "loc": 0, "scale": 1}
             tr = CLEARVAETrainer(vae, opt, "cosine", hp, 1, dev)
+        elif mode == "group":
+            tr = HierarchicalVAETrainer(vae, opt, {"beta": 0.125, "loc": 0, "scale": 1}, 1, dev)
+        elif mode == "tc":
+            hp = {"temperature": 0.1, "beta": 0.125, "loc": 0, "scale": 1, "alpha": 100.0, "lambda": 3.0}
+            disc = torch.nn.Sequential(torch.nn.Linear(zt, zt), torch.nn.ReLU(), torch.nn.Linear(zt, 1),
+                                       torch.nn.Sigmoid()).cuda()
+            dd = R.det_disc(zt)
+            if rank != 0:
+                dd = {k: v * 0.5 for k, v in dd.items()}
+            disc.load_state_dict({k: torch.tensor(v, dtype=torch.float32) for k, v in dd.items()})
+            fopt = torch.optim.Adam(disc.parameters(), lr=1e-3)
+            tr = ClearTCVAETrainer(vae, disc, {"vae_optim": opt, "factor_optim": fopt}, "cosine", hp, 1, dev)
         else:
             hp = {"temperature": 0.1, "beta": 0.125, "loc": 0, "scale": 1, "alpha": 100.0, "lambda": 3.0}
             est = (CLUBSample if kind == "CLUBSample" else L1OutUB)(zt // 2, zt // 2, zt).cuda()
@@ -63,7 +75,7 @@ def run(rank, world, port, q, mode, n_global, kind):
         eng = ClearStep.build(tr, mode)
         assert eng is not None and eng.world == world, "fused DP engine not built"
         out = {"p0": {k: _np(v) for k, v in vae.state_dict().items() if "running" not in k and "num_b" not in k}}
-        if mode == "mim":
+        if mode in ("mim", "tc"):
             out["e0"] = _np(eng.est_arena.flat)
 
         # step 1: injected noise (eager segments), this rank's contiguous shard of the global batch
@@ -73,6 +85,13 @@ def run(rank, world, port, q, mode, n_global, kind):
         rng.clear_injections()
         if mode == "clear":
             rng.inject_noise([torch.tensor(ec[lo:hi], dtype=torch.float32), torch.tensor(es[lo:hi], dtype=torch.float32)])
+        elif mode == "group":  # content noise rows in this shard's group order
+            rng.inject_noise([R.group_order_noise(label[lo:hi], torch.tensor(ec[lo:hi])).float(),
+                              torch.tensor(es[lo:hi], dtype=torch.float32)])
+        elif mode == "tc":
+            gen = np.random.default_rng(6)
+            a2, b2 = gen.standard_normal((n_global, zt // 2)), gen.standard_normal((n_global, zt // 2))
+            rng.inject_noise([torch.tensor(t[lo:hi], dtype=torch.float32) for t in (ec, es, a2, b2)])
         else:
             gen = np.random.default_rng(5)
             noises = [(ec, es)] + [(gen.standard_normal((n_global, zt // 2)), gen.standard_normal((n_global, zt // 2)))
@@ -85,7 +104,7 @@ def run(rank, world, port, q, mode, n_global, kind):
         L = torch.tensor(label[lo:hi], device=dev)
         res = eng.step(X, L)
         torch.cuda.synchronize()
-        if mode == "clear":
+        if mode in ("clear", "group"):
             out["losses"] = _np(res)
         else:
             out["losses"], out["learn"] = _np(res[0]), _np(res[1])
@@ -102,7 +121,7 @@ def run(rank, world, port, q, mode, n_global, kind):
         torch.cuda.synchronize()
         out["graphs"] = "graphs" in eng.graphs[n]
         out["p3"] = _np(eng.arena.flat)
-        if mode == "mim":
+        if mode in ("mim", "tc"):
             out["e3"] = _np(eng.est_arena.flat)
         eng.sync_host_state()
         out["opt_step"] = int(float(opt.state[next(vae.parameters())]["step"]))

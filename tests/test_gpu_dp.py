@@ -8,7 +8,9 @@ processes on the one GPU over gloo (tests/dp_gpu_worker.py), against the DDP sem
   * the parameters after Adam are identical (bitwise) across ranks, equal to torch Adam applied to that
     mean gradient, and stay identical through graph-captured replays;
   * CLEAR-MIM: the estimator's 5 updates use the mean of the per-shard learning-loss gradients, and the
-    estimator parameters are identical across ranks.
+    estimator parameters are identical across ranks;
+  * CLEAR-TC: the discriminator's BCE gradients are averaged the same way, its parameters identical across
+    ranks; GVAE / ML-VAE: each rank's group evidence is over its own shard (the groups of its local batch).
 
 Tolerances are those of tests/test_gpu_parity.py (losses 1e-4 relative, gradient checks of
 `_check_grads`, Adam-step parameter checks)."""
@@ -179,6 +181,92 @@ def test_dp_mim_step_world2(kind):
     for k in ("p_mu.0.weight", "p_mu.0.bias", "p_mu.2.weight", "p_mu.2.bias", "p_logvar.0.weight", "p_logvar.0.bias",
               "p_logvar.2.weight", "p_logvar.2.bias"):
         nel = Md[k].numel()
+        got_e.append(torch.tensor(e1[o:o + nel]))
+        o = (o + nel + 3) & ~3
+    assert _rel(torch.cat(got_e), ref_e) < 1e-3
+
+
+@pytest.mark.parametrize("kind", ["GVAE", "MLVAE"])
+def test_dp_group_step_world2(kind):
+    from oracle import cpu_ref as R
+
+    n_global, zt = 64, 16
+    res = _launch("group", n_global, kind)
+    sd = R.det_state("VAE", zt, 1)
+    _common_checks(res, sd)
+    hp = {"beta": 0.125, "loc": 0, "scale": 1}
+    x, label, ec, es, _ = R.det_inputs(n_global, 1, 28, zt, 4, seed=21)
+    shards = []
+    for r in (0, 1):
+        lo, hi = res[r]["bounds"]
+        o = R.group_step(R.to_torch(sd), torch.tensor(x[lo:hi]), torch.tensor(label[lo:hi]),
+                         R.group_order_noise(label[lo:hi], torch.tensor(ec[lo:hi])), torch.tensor(es[lo:hi]), "VAE",
+                         hp, kind)
+        shards.append(o)
+        got = res[r]["losses"]
+        for i, k in ((0, "rec_adj"), (1, "kl_c"), (2, "kl_s_adj")):
+            ref = float(o[k])
+            assert abs(float(got[i]) - ref) <= LOSS_TOL * max(abs(ref), 1e-3), (r, k, float(got[i]), ref)
+    mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
+    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, "VAE")
+    ref_p = _adam_ref(sd, mean_g)
+    prel = sorted((_rel(res[0]["p1"][k], ref_p[k]), k) for k in ref_p)
+    assert prel[len(prel) // 2][0] < 1e-5, prel[-3:]
+    assert prel[-1][0] < 5e-3, prel[-3:]
+
+
+def test_dp_tc_step_world2():
+    from oracle import cpu_ref as R
+
+    n_global, zt = 64, 16
+    res = _launch("tc", n_global)
+    sd = R.det_state("VAE", zt, 1)
+    _common_checks(res, sd)
+    for key in ("e0", "e1", "e3"):
+        assert np.array_equal(res[0][key], res[1][key]), key
+    hp = {"temperature": 0.1, "beta": 0.125, "loc": 0, "scale": 1, "alpha": 100.0, "lambda": 3.0}
+    x, label, ec, es, _ = R.det_inputs(n_global, 1, 28, zt, 4, seed=21)
+    gen = np.random.default_rng(6)
+    a2, b2 = gen.standard_normal((n_global, zt // 2)), gen.standard_normal((n_global, zt // 2))
+    D0 = R.to_torch(R.det_disc(zt))
+    shards = []
+    for r in (0, 1):
+        lo, hi = res[r]["bounds"]
+        o = R.tc_step(R.to_torch(sd), D0, torch.tensor(x[lo:hi]), torch.tensor(label[lo:hi]), torch.tensor(ec[lo:hi]),
+                      torch.tensor(es[lo:hi]), "VAE", hp)
+        shards.append(o)
+        got = res[r]["losses"]
+        for i, k in ((0, "rec"), (1, "kl_c"), (2, "kl_s"), (3, "c_loss")):
+            ref = float(o[k].detach())
+            assert abs(float(got[i]) - ref) <= LOSS_TOL * max(abs(ref), 1e-3), (r, k, float(got[i]), ref)
+        mi = float(o["mi"].detach())
+        assert abs(float(got[5]) - mi) <= LOSS_TOL * max(abs(mi), 1.0), (r, float(got[5]), mi)
+    mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
+    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, "VAE")
+    # the discriminator step: per-shard BCE on z of the second forward (fresh noise, post-Adam VAE), gradients
+    # averaged over the shards, torch Adam
+    P1 = R.to_torch(sd, requires_grad=False)
+    P1.update(_adam_ref(sd, mean_g))
+    Dp = [v.detach().clone().requires_grad_(True) for v in D0.values()]
+    Dd = dict(zip(D0.keys(), Dp))
+    grads = None
+    for r in (0, 1):
+        lo, hi = res[r]["bounds"]
+        P = {k: (v.clone() if ("running" in k or "num_batches" in k) else v) for k, v in P1.items()}
+        with torch.no_grad():
+            _, _, z2 = R.vae_forward(P, torch.tensor(x[lo:hi]), torch.tensor(a2[lo:hi]), torch.tensor(b2[lo:hi]),
+                                     "VAE", True)
+        fl = R.tc_factor_loss(Dd, z2)
+        assert abs(float(res[r]["learn"][0]) - float(fl)) <= 1e-3 * abs(float(fl)), (r, float(res[r]["learn"][0]))
+        g = torch.autograd.grad(fl, Dp)
+        grads = [gi / 2 for gi in g] if grads is None else [acc + gi / 2 for acc, gi in zip(grads, g)]
+    for p_, g in zip(Dp, grads):
+        p_.grad = g
+    torch.optim.Adam(Dp, lr=1e-3).step()
+    ref_e = torch.cat([Dd[k].detach().reshape(-1) for k in ("0.weight", "0.bias", "2.weight", "2.bias")])
+    e1, got_e, o = res[0]["e1"], [], 0
+    for k in ("0.weight", "0.bias", "2.weight", "2.bias"):
+        nel = Dd[k].numel()
         got_e.append(torch.tensor(e1[o:o + nel]))
         o = (o + nel + 3) & ~3
     assert _rel(torch.cat(got_e), ref_e) < 1e-3
