@@ -491,7 +491,10 @@ struct StepRedArgs {
   int nplain;
   int nprod;  // blocks that reduce the deferred segments (grid-stride over blk0[nd] segments)
 };
-constexpr int SR_E = 64;           // partial-tile elements per block: 256-byte row segments
+#ifndef CV_SR_E
+#define CV_SR_E 128
+#endif
+constexpr int SR_E = CV_SR_E;      // partial-tile elements per block: 256-byte row segments
 constexpr int SR_G = 256 / SR_E;   // split groups per element (each thread sums every SR_G-th split)
 
 // torch.optim.Adam (foreach) on one element of the arena, constants from adam_consts

@@ -1171,6 +1171,12 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
     }
   }
   a.kchunk = w.kchunk;
+  static int atomic_splits = -1;  // A/B knob CV_WGRAD_ATOMIC=1: split-K tiles added with fp32 atomics, no partials
+  if (atomic_splits < 0) {
+    const char* e = getenv("CV_WGRAD_ATOMIC");
+    atomic_splits = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  if (atomic_splits) work = nullptr;
   if (w.split > 1 && work) {
     const size_t need = (size_t)w.split * a.M * Ntot * sizeof(float);
     CV_REQUIRE(work_bytes >= need, "wgrad: workspace %zu bytes < %zu needed", work_bytes, need);
