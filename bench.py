@@ -455,6 +455,14 @@ def pipeline_pass(device, n=1024, hw=96, out=64, reps=50, cpu_budget_s=3.0):
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
                         "frac": round(gbs / PEAK_HBM_GBS, 4), "unit": "GB/s", "traffic": None,
                         "bytes_per_image": per_img}}
+    # HBM bytes per launch from the committed PMC passes of the same launch (scratch/pipe_pmc.py,
+    # profiles/pmc_traffic.py): taken at this shape only
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "pipeline_traffic.json")))["calls"]
+        if n == 1024 and hw == 96 and out == 64:
+            rec["roofline"]["traffic"] = round(float(t["load_batch_u8:camelyon96_bs1024"]["traffic_bytes"]))
+    except (OSError, ValueError, KeyError):
+        pass
     try:
         from PIL import Image
 
