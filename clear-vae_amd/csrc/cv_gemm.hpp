@@ -137,29 +137,70 @@ __device__ __forceinline__ void fill_soa(const cv_bn& bn, int nf, float* dst, do
 // Finalised constants of a train-mode layer (cv_bn.cfwd / cbwd, written by the producer's last
 // workgroup): a float4 copy into LDS instead of the replica fold.  The SoA order of cfwd starts with
 // [sc][mu][beta] and cbwd is [sc][c1][mu][istd][c2], exactly the LDS images above.
+// Split in two phases so every constant set of a prologue (A transform, B transform, the STAT_BWD
+// epilogue's forward constants) is in flight together with the first tile's loads and the prologue pays
+// ONE memory round trip: soa_issue loads the constants and the ticket into registers (nothing waits),
+// soa_commit checks the ticket and writes LDS (a zero ticket: the producer did not finalise, and the
+// caller folds the replica sums instead).
+struct SoaPre {
+  f32x4 tmp[3];
+  unsigned tk;
+  bool ok;
+};
 template <int XF>
-__device__ __forceinline__ bool load_soa(const cv_bn& bn, int nf, float* dst) {
+__device__ __forceinline__ SoaPre soa_issue(const cv_bn& bn, int nf) {
+  SoaPre p;
   const float* src = (XF == CV_XF_BNRELU) ? bn.cfwd : bn.cbwd;
-  if (!bn.train || !src || !bn.ticket || nf != bn.C) return false;
-  // the constant loads are issued with the ticket load (a zero ticket: the producer did not
-  // finalise, and the fold runs instead)
-  constexpr int MQ4 = 3;
+  p.ok = bn.train && src && bn.ticket && nf == bn.C;
+  p.tk = 0u;
+  if (!p.ok) return p;
   const int n4 = soa_arrays<XF>() * nf / 4;
   const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
-  f32x4 tmp[MQ4];
 #pragma unroll
-  for (int q = 0; q < MQ4; ++q) {
+  for (int q = 0; q < 3; ++q) {
     const int i = threadIdx.x + q * NT;
-    tmp[q] = s4[i < n4 ? i : 0];
+    p.tmp[q] = s4[i < n4 ? i : 0];
   }
-  if (bn.ticket[XF == CV_XF_BNRELU ? 0 : 1] == 0u) return false;
+  p.tk = bn.ticket[XF == CV_XF_BNRELU ? 0 : 1];
+  return p;
+}
+template <int XF>
+__device__ __forceinline__ bool soa_commit(const SoaPre& p, const cv_bn& bn, int nf, float* dst) {
+  if (!p.ok || p.tk == 0u) return false;
+  const float* src = (XF == CV_XF_BNRELU) ? bn.cfwd : bn.cbwd;
+  const int n4 = soa_arrays<XF>() * nf / 4;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
   f32x4* d4 = reinterpret_cast<f32x4*>(dst);
 #pragma unroll
-  for (int q = 0; q < MQ4; ++q) {
+  for (int q = 0; q < 3; ++q) {
     const int i = threadIdx.x + q * NT;
-    if (i < n4) d4[i] = tmp[q];
+    if (i < n4) d4[i] = p.tmp[q];
   }
-  for (int i = threadIdx.x + MQ4 * NT; i < n4; i += NT) d4[i] = s4[i];
+  for (int i = threadIdx.x + 3 * NT; i < n4; i += NT) d4[i] = s4[i];
+  return true;
+}
+// the STAT_BWD epilogue's forward constants (AoS BnFwdC in LDS) from cfwd = [sc][mu][beta][istd]
+struct EpiPre {
+  float v[4];
+  unsigned tk;
+  bool ok;
+};
+__device__ __forceinline__ EpiPre epi_issue(const cv_bn& eb, int ce_n) {
+  EpiPre p;
+  p.ok = eb.train && eb.cfwd && eb.ticket && eb.C == ce_n;
+  p.tk = 0u;
+  if (!p.ok) return p;
+  const int f = (int)threadIdx.x < ce_n ? (int)threadIdx.x : 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p.v[q] = eb.cfwd[q * eb.C + f];
+  p.tk = eb.ticket[0];
+  return p;
+}
+__device__ __forceinline__ bool epi_commit(const EpiPre& p, const cv_bn& eb, int ce_n, BnFwdC* d) {
+  if (!p.ok || p.tk == 0u) return false;
+  if ((int)threadIdx.x < ce_n) d[threadIdx.x] = BnFwdC{p.v[0], p.v[1], p.v[2], p.v[3]};
+  for (int f = threadIdx.x + NT; f < ce_n; f += NT)
+    d[f] = BnFwdC{eb.cfwd[f], eb.cfwd[eb.C + f], eb.cfwd[2 * eb.C + f], eb.cfwd[3 * eb.C + f]};
   return true;
 }
 
@@ -593,6 +634,13 @@ void gemm_kernel(const Args P) {
   if (false)  // diagnostic build: no constants fold (garbage constants)
 #endif
   {
+  // every finalised constant set is requested before the first wait (one round trip with the tile loads)
+  SoaPre pa{}, pb{};
+  EpiPre pe{};
+  if constexpr (XA != CV_XF_NONE) {
+    if (!bn1d) pa = soa_issue<XA>(P.a.bn, nfa);
+  }
+  if constexpr (EPI == CV_STAT_BWD) pe = epi_issue(P.ep.ebn, P.ce_n);
   if constexpr (XA != CV_XF_NONE) {
     if (bn1d) {
       const float* src = (XA == CV_XF_BNRELU) ? P.a.bn.cfwd : P.a.bn.cbwd;
@@ -620,26 +668,18 @@ void gemm_kernel(const Args P) {
           cA[4 * nfa + idx] = k.c2;
         }
       }
-    } else if (!load_soa<XA>(P.a.bn, nfa, cA)) {
+    } else if (!soa_commit<XA>(pa, P.a.bn, nfa, cA)) {
       fill_soa<XA>(P.a.bn, nfa, cA, fold_scratch);
     }
   }
-  if constexpr (XFB != CV_XF_NONE) {
-    if (!load_soa<XFB>(P.b.bn, nfb, cB)) fill_soa<XFB>(P.b.bn, nfb, cB, fold_scratch);
+  if constexpr (XFB != CV_XF_NONE) {  // WGRAD only (long K): issued after A's commit, fewer live registers
+    pb = soa_issue<XFB>(P.b.bn, nfb);
+    if (!soa_commit<XFB>(pb, P.b.bn, nfb, cB)) fill_soa<XFB>(P.b.bn, nfb, cB, fold_scratch);
   }
   if constexpr (EPI == CV_STAT_BWD) {
     BnFwdC* d = reinterpret_cast<BnFwdC*>(cE);
     const cv_bn& eb = P.ep.ebn;
-    if (eb.train && eb.cfwd && eb.ticket && eb.C == P.ce_n && eb.ticket[0] != 0u) {
-      for (int f = t; f < P.ce_n; f += NT) {
-        BnFwdC k;
-        k.sc = eb.cfwd[f];
-        k.mu = eb.cfwd[eb.C + f];
-        k.be = eb.cfwd[2 * eb.C + f];
-        k.istd = eb.cfwd[3 * eb.C + f];
-        d[f] = k;
-      }
-    } else {
+    if (!epi_commit(pe, eb, P.ce_n, d)) {
       bn_fold<NT>(eb, false, fold_scratch, [&](int f, double s, double q, double, double) {
         if (f < P.ce_n) d[f] = bn_fwd_const_s(eb, f, s, q);
       });
