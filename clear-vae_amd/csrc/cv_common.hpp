@@ -256,6 +256,9 @@ __device__ __forceinline__ void bn_fold(const cv_bn& b, bool with_g, double* scr
 template <int NT>
 __device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, bool bwd, double* scratch, int* flag) {
   float* out = bwd ? b.cbwd : b.cfwd;
+#ifdef CV_NO_FINALIZE  // A/B build: no producer-side finalisation (every consumer folds the replicas)
+  return;
+#endif
   if (!b.ticket || !out || !b.train || !produced) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -143,19 +143,38 @@ __device__ __forceinline__ void combine_body(const CombineArgs& C, double* scrat
   const float w = (float)((double)beta / (1.0 + exp(-(t - (double)loc) / (double)scale)));
   const float inv_n = 1.0f / (float)n;
   double sc = 0.0, ss = 0.0;
-  const int zd = 2 * d;
-  for (int e = threadIdx.x; e < n * zd; e += NTH) {
-    const int r = e / zd, j = e % zd;
-    const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
-    const float m = heads[(size_t)r * 4 * d + blk * d + k];
-    const float l = heads[(size_t)r * 4 * d + (blk + 1) * d + k];
-    const float el = expf(l);
-    const double term = (double)(1.0f + l - m * m - el);
-    if (j < d) sc += term; else ss += term;
-    const float g = dz ? dz[e] : 0.f;
-    const float zz = z[e];
-    dheads[(size_t)r * 4 * d + blk * d + k] = w * m * inv_n + g;
-    dheads[(size_t)r * 4 * d + (blk + 1) * d + k] = w * (-0.5f * inv_n) * (1.0f - el) + g * (zz - m) * 0.5f;
+  const int zd = 2 * d, total = n * zd;
+  // one workgroup walks n x 2d elements: batches of U elements per thread have all their loads in
+  // flight before the first use (one memory latency per batch instead of one per element: 64 serial
+  // latencies per thread at VAE64 bs=256).  Each thread still visits e = t, t + NTH, ... in order, so
+  // the fp64 KL sums are bit-identical to the element-at-a-time loop.
+  constexpr int U = 8;
+  for (int base = threadIdx.x; base < total; base += NTH * U) {
+    float m[U], l[U], g[U], zz[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = base + q * NTH;
+      const int ec = e < total ? e : 0;
+      const int r = ec / zd, j = ec - r * zd;
+      const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
+      m[q] = heads[(size_t)r * 4 * d + blk * d + k];
+      l[q] = heads[(size_t)r * 4 * d + (blk + 1) * d + k];
+      g[q] = dz ? dz[ec] : 0.f;
+      zz[q] = z[ec];
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = base + q * NTH;
+      if (e >= total) break;
+      const int r = e / zd, j = e - r * zd;
+      const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
+      const float el = expf(l[q]);
+      const double term = (double)(1.0f + l[q] - m[q] * m[q] - el);
+      if (j < d) sc += term; else ss += term;
+      dheads[(size_t)r * 4 * d + blk * d + k] = w * m[q] * inv_n + g[q];
+      dheads[(size_t)r * 4 * d + (blk + 1) * d + k] =
+          w * (-0.5f * inv_n) * (1.0f - el) + g[q] * (zz[q] - m[q]) * 0.5f;
+    }
   }
   const double kc = block_sum<NTH>(sc, scratch);
   const double ks = block_sum<NTH>(ss, scratch);
@@ -543,7 +562,47 @@ __device__ __forceinline__ void ntl_stage(const Branch& b, const int64_t* label,
   // batches of 8 loads in flight per thread before the LDS writes (one latency per batch)
   constexpr int U = 8;
   const int nd = n * d;
-  for (int base = t; base < nd; base += 256 * U) {
+  // the labels / row log-sum-exps of this thread's first rows are requested first, so the wait of the
+  // first row batch covers them too
+  constexpr int UL = 2;
+  long long lb0[UL];
+  float la0[UL], lp0[UL];
+#pragma unroll
+  for (int q = 0; q < UL; ++q) {
+    const int i = t + q * 256;
+    lb0[q] = (i < n) ? label[i] : 0;
+    la0[q] = (grad && i < n) ? b.lse[i] : 0.f;
+    lp0[q] = (grad && i < n) ? b.lse[n + i] : 0.f;
+  }
+  // float4 rows when the branch is 16-byte aligned (every VAE / VAE64 head block): n x d/4 vector loads,
+  // one batch of U per thread covers n*d <= 8192 (MNIST bs=512 d=8, VAE64 bs=256 d=32) in one latency
+  const bool vec = (d % 4 == 0) && (b.ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(b.mu) & 15) == 0) &&
+                   (!need_lv || (reinterpret_cast<uintptr_t>(b.lv) & 15) == 0);
+  const int d4 = d / 4, nq = vec ? n * d4 : 0;
+  const FDiv fd4 = FDiv::make(vec ? d4 : 1);
+  for (int base = t; base < nq; base += 256 * U) {
+    f32x4 vm[U], vl[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = base + q * 256, ic = i < nq ? i : 0;
+      const int r = fd4.div(ic), k4 = ic - r * d4;
+      vm[q] = *reinterpret_cast<const f32x4*>(b.mu + (size_t)r * b.ld + 4 * k4);
+      vl[q] = need_lv ? *reinterpret_cast<const f32x4*>(b.lv + (size_t)r * b.ld + 4 * k4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = base + q * 256;
+      if (i < nq) {
+        const int r = fd4.div(i), k4 = i - r * d4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          L.mu[r * pd + 4 * k4 + c] = vm[q][c];
+          if (need_lv) L.lv[r * pd + 4 * k4 + c] = vl[q][c];
+        }
+      }
+    }
+  }
+  for (int base = vec ? nd : t; base < nd; base += 256 * U) {
     float vm[U], vl[U];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
@@ -562,7 +621,18 @@ __device__ __forceinline__ void ntl_stage(const Branch& b, const int64_t* label,
       }
     }
   }
-  for (int base = t; base < n; base += 256 * U) {
+#pragma unroll
+  for (int q = 0; q < UL; ++q) {
+    const int i = t + q * 256;
+    if (i < n) {
+      L.lab[i] = lb0[q];
+      if (grad) {
+        L.lse[i] = la0[q];
+        L.lse[n + i] = lp0[q];
+      }
+    }
+  }
+  for (int base = t + UL * 256; base < n; base += 256 * U) {
     long long lb[U];
     float la[U], lp[U];
 #pragma unroll
