@@ -21,7 +21,9 @@ After the timed region (nothing below is inside it):
       torch-CPU) on a bounded sample, and the ELBO (and, for CLEAR-MIM, MI) error of one HIP step against
       the fp64 CPU reference on the same batch / weights / noise;
   (3) default config at N=1: configs[2] (CelebA 64x64 bs=256 CLEAR-MIM CLUB-S) is timed the same way
-      and reported under "c3";
+      and reported under "c3"; the per-GPU shards of configs[3] (PACS, VAE64 bs=32 fp32) and configs[4]
+      (Camelyon17, VAE64 bs=128 bf16) are timed on this one GPU under "c4_per_gpu" / "c5_per_gpu"
+      (img/s of one rank; their DDP totals are the driver's multi-GPU runs);
   (4) default / camelyon-bf16 config at N=1: the device input pipeline (Resize((64, 64)) + ToTensor of a
       96x96x3 uint8 batch of 1024, cv_load_batch_u8) under "input_pipeline", with Pillow's own transform
       timed beside it on one host core.
@@ -54,6 +56,10 @@ CONFIGS = {
                    dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, la=3.0, mi_lr=2e-3), "CLUBSample"),
     "celeba": ("VAE64", 64, 3, 64, 256, "clear", 4,
                dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, ps=True), None),
+    # configs[3]: PACS resized to 64x64 before the model (code/run_pacs_downstream_expr.py:88-98), bs=128
+    # over 4 GPUs = 32 per GPU, fp32; 7 domains' labels
+    "pacs": ("VAE64", 64, 3, 64, 32, "clear", 7,
+             dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, ps=True), None),
     # configs[4]: Camelyon17 patches resized to 64x64 before the model, bs=1024 over 8 GPUs =
     # 128 per GPU, bf16 contractions
     "camelyon-bf16": ("VAE64", 64, 3, 64, 128, "clear", 2,
@@ -544,6 +550,14 @@ def main():
               "config": workload_label("celeba-mim", ccfg, 1),
               "algorithmic_tflops": round(r3["algorithmic_tflops"], 3), "losses_finite": r3["finite"],
               "roofline": r3.get("roofline")}
+        shards = {}
+        for key, cname in (("c4_per_gpu", "pacs"), ("c5_per_gpu", "camelyon-bf16")):
+            ccfg = CONFIGS[cname]
+            r = run_workload(cname, ccfg, min(args.steps, 100), 10, device, 1, 0, detail=False)
+            shards[key] = {"value": round(r["value"], 1), "unit": "images/s", "ms_per_step": round(r["ms_per_step"], 4),
+                           "steps": min(args.steps, 100), "dtype": ccfg[7].get("precision", "fp32"),
+                           "config": workload_label(cname, ccfg, 1), "losses_finite": r["finite"],
+                           "algorithmic_tflops": round(r["algorithmic_tflops"], 3)}
     if rank == 0:
         rec = {
             "metric": "training images/sec at bs=512; ELBO rel-err vs CPU ref",
@@ -575,6 +589,7 @@ def main():
                 except Exception as e:  # pragma: no cover
                     c3["elbo_rel_err"] = repr(e)
                 rec["c3"] = c3
+                rec.update(shards)
             if args.config in ("mnist", "camelyon-bf16") and args.batch is None:
                 try:
                     rec["input_pipeline"] = pipeline_pass(device)
