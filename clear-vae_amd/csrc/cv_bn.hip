@@ -537,6 +537,20 @@ __device__ __forceinline__ void defer_segment(const StepRedArgs& a, const AdamC&
     const long o = (long)(b - a.blk0[di]) * SR_E + ol;
     const long total = (long)d.M * d.ntot;
     const size_t sstride = (size_t)total;
+    // the destination of this thread's element (threads < SR_E) is resolved and its current value
+    // requested first, so the read-modify-write costs no extra latency after the reduction
+    float* dst = nullptr;
+    float old = 0.f;
+    if (t < SR_E && o < total) {
+      const int row = (int)(o / d.ntot), col = (int)(o - (long)row * d.ntot);
+      if (col < d.N) {
+        const int tap = col / d.cb, c = col - tap * d.cb;
+        dst = d.gweight + ((size_t)row * d.cb + c) * d.kk + tap;
+      } else if (d.gbias) {
+        dst = d.gbias + row;
+      }
+      if (dst) old = *dst;
+    }
     float acc = 0.f;
     if (o < total) {
       const float* p = d.part + o;
@@ -547,27 +561,26 @@ __device__ __forceinline__ void defer_segment(const StepRedArgs& a, const AdamC&
         for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(z + u * SR_G) * sstride];
         acc += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
       }
-      for (; z < d.split; z += SR_G) acc += p[(size_t)z * sstride];
+      // the < 8 remaining slices: every load issued before the first add (the adds keep the serial order;
+      // absent slices add an exact 0)
+      float v[7];
+#pragma unroll
+      for (int u = 0; u < 7; ++u) {
+        const int zz = z + u * SR_G;
+        v[u] = (zz < d.split) ? p[(size_t)zz * sstride] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 7; ++u) acc += v[u];
     }
     red[zg][ol] = acc;
     __syncthreads();
-    if (t < SR_E && o < total) {
+    if (dst) {
       float v = 0.f;
 #pragma unroll
       for (int g = 0; g < SR_G; ++g) v += red[g][t];  // fixed order: deterministic
-      const int row = (int)(o / d.ntot), col = (int)(o - (long)row * d.ntot);
-      float* dst = nullptr;
-      if (col < d.N) {
-        const int tap = col / d.cb, c = col - tap * d.cb;
-        dst = d.gweight + ((size_t)row * d.cb + c) * d.kk + tap;
-      } else if (d.gbias) {
-        dst = d.gbias + row;
-      }
-      if (dst) {
-        const float g = *dst + v;
-        *dst = g;
-        if (adam) adam_elem(a, ac, dst - a.ag, g);
-      }
+      const float g = old + v;
+      *dst = g;
+      if (adam) adam_elem(a, ac, dst - a.ag, g);
     }
     __syncthreads();  // (red is reused by the block's next segment)
   }
