@@ -513,9 +513,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL over xGMI; CV_DIST_BACKEND=gloo rehearses the multi-rank flow with several ranks on one GPU
+    backend = os.environ.get("CV_DIST_BACKEND", "nccl")
+    if world > 1 and backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     cfg = list(CONFIGS[args.config])
