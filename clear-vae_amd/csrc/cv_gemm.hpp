@@ -20,6 +20,7 @@
 //     reads at store time) AFTER the first tiles' loads are issued, so the fold's latency hides
 //     under them.
 #pragma once
+#include <stdlib.h>
 #include "cv_igemm.hpp"
 
 namespace cv {
@@ -239,669 +240,26 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
 __global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? CV_FAST_MINW_SMALL : (BM == 64 ? CV_FAST_MINW_64 : 1))
 void gemm_kernel(const Args P) {
-  static_assert(D >= 2, "the register ring needs at least two stages (D=1 is not a valid schedule)");
-  using SH = Shape<OP, BM, BN>;
-  constexpr int WN = SH::WN, WM = SH::WM, TM = SH::TM, TN = SH::TN, FM = SH::FM, FN = SH::FN;
-  constexpr int RA = SH::RA, RB = SH::RB;
-  static_assert(FM >= 1 && FN >= 1 && RA >= 1, "tile too small");
-  constexpr bool ROWS = OP != OP_WGRAD;
-  constexpr int XFB = (OP == OP_WGRAD) ? XB : CV_XF_NONE;  // B transform (WGRAD only)
-  constexpr bool AY = XA == CV_XF_BNBWD, BYY = XFB == CV_XF_BNBWD;
-  constexpr int DBM = (OP == OP_DENSE) ? XB : DB_NCONT;    // B staging mode
-  constexpr bool BKC = (DBM == DB_KCONT || DBM == DB_KPERM);
-  // quad-transposed staging of the non-k-contiguous B operand (CV_FAST_QTB=1); off by default: it makes
-  // every B load instruction touch twice the cache lines and measured slower on the forward / backward-data
-  // GEMMs, while the WGRAD A operand (worst conflicts) always uses it
-  constexpr bool QTB = (CV_FAST_QTB != 0) && !BKC;
+#include "cv_gemm_prelude.inc"
 
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;                       // [2][BM][LDK]
-  float* Bs = As + 2 * BM * LDK;          // [2][BN][LDK]
-  float* red = Bs + 2 * BN * LDK;         // [2][WM][BN]
-  // bf16 images live at the start of the same regions ([2][BM][LDKH] / [2][BN][LDKH] halves)
-  __bf16* Ah = reinterpret_cast<__bf16*>(As);
-  __bf16* Bh = reinterpret_cast<__bf16*>(Bs);
-  const bool bn1d = (OP == OP_DENSE) && XA != CV_XF_NONE && P.ca_n == P.K;
-  const int nfa = (XA == CV_XF_NONE) ? 0 : (bn1d ? P.kchunk : P.ca_n);
-  const int nfb = (XFB == CV_XF_NONE) ? 0 : P.cb_n;
-  float* cA = red + 2 * WM * BN;
-  float* cB = cA + soa_arrays<XA>() * nfa;
-  float* cE = cB + soa_arrays<XFB>() * nfb;  // STAT_BWD: BnFwdC of the epilogue's BN layer
-
-  CV_STAMP(st0);
-#ifdef CV_STAMPS
-  const unsigned long long mt0 = __builtin_amdgcn_s_memtime();
-#endif
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const Geo& g = P.g;
-
-  // producer side of the BN constants hand-off: every workgroup arrives once (early exits too)
-  auto finalize = [&](bool) {
-    if constexpr (EPI != CV_STAT_NONE) {
-      bn_finalize<NT>(P.ep.ebn, P.ep.stat_out, EPI == CV_STAT_BWD, reinterpret_cast<double*>(As),
-                      reinterpret_cast<int*>(As + 4096));
-    }
-  };
-
-  // ---------------- block -> (m0, n0, k-range, class): identical to the generic kernel
+  // ---------------- one tile per workgroup
   const int gx = gridDim.x, gy = gridDim.y;
   const int nwg = gx * gy * gridDim.z;
   const int hw_id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (OP == OP_WGRAD) {
-    const int xcd = hw_id & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (hw_id >> 3);
-    by = lid % gy;
-    bx = (lid / gy) % gx;
-    bz = lid / (gx * gy);
-  }
-  const int m0 = bx * BM, n0 = by * BN;
-  int M = P.M, K = P.K;
-  const int N = P.N + ((OP == OP_WGRAD && P.gbias) ? 1 : 0);
-  int kbeg = 0, kend = K;
-  int ry = 0, rx = 0, yb0 = 0, xb0 = 0, cy = 1, cx = 1, ntx = 1;
-  FDiv f_cx = FDiv::make(1), f_cycx = FDiv::make(1), f_ntx = FDiv::make(1);
-  if (OP == OP_SCATTER) {
-    const int s = g.s, cls = bz;
-    ry = cls / s;
-    rx = cls % s;
-    yb0 = (((ry - g.p) % s) + s) % s;
-    xb0 = (((rx - g.p) % s) + s) % s;
-    cy = (g.hb > yb0) ? (g.hb - yb0 + s - 1) / s : 0;
-    cx = (g.wb > xb0) ? (g.wb - xb0 + s - 1) / s : 0;
-    const int nty = (g.kh > ry) ? (g.kh - ry + s - 1) / s : 0;
-    ntx = (g.kw > rx) ? (g.kw - rx + s - 1) / s : 0;
-    M = g.n * cy * cx;
-    K = nty * ntx * g.cs;
-    kend = K;
-    if (m0 >= M) {
-      finalize(true);
-      return;
-    }
-    f_cx = FDiv::make(cx);
-    f_cycx = FDiv::make(cy * cx);
-    f_ntx = FDiv::make(ntx);
-  } else {
-    kbeg = bz * P.kchunk;
-    kend = min(K, kbeg + P.kchunk);
-    if (kbeg >= kend) {
-      finalize(true);
-      return;
-    }
-  }
-  const int nt = (kend - kbeg + BK - 1) / BK;
-  // GATHER / SCATTER visit K tiles tap-inner: tile j = (channel block j / ntap, tap j % ntap), so a
-  // thread's channel quad (and its BN constants) changes only every ntap tiles
-  const int ntap = (OP == OP_GATHER) ? g.kh * g.kw : (OP == OP_SCATTER ? (ntx > 0 ? K / g.cs : 1) : 1);
-  const FDiv f_ntap = FDiv::make(ntap);
-  const int CK = (OP == OP_GATHER) ? g.cb : g.cs;  // channels per tap of the K index
-
-  // ---------------- per-thread A rows (row-oriented ops): rows (t>>3) + 32 i, k quad t & 7.
-  // GATHER / SCATTER: a K tile never straddles a tap (channels % BK == 0, checked on the host), so
-  // the tap of a tile is wave-uniform (scalar unit); per row we keep the element offset of tap 0,
-  // channel 0 (r_base, may be negative for padded rows) and a bitmask of the taps that land inside
-  // the image (r_vm), so a tile costs one add and one bit test per row.
-  const int aq = t & 7, ar = t >> 3;
-  int r_base[RA];
-  unsigned r_vm[RA];
-  int cy0 = 0, cx0 = 0;
-  if constexpr (OP == OP_SCATTER) {
-    cy0 = (yb0 + g.p - ry) / g.s;  // small row of class tap jy = 0 is cy0 + ty (exact division)
-    cx0 = (xb0 + g.p - rx) / g.s;
-  }
-  if constexpr (ROWS) {
-#pragma unroll
-    for (int i = 0; i < RA; ++i) {
-      const int r = m0 + ar + 32 * i;
-      const bool ok = r < M;
-      const int rr = ok ? r : 0;
-      unsigned vm = 0;
-      if constexpr (OP == OP_GATHER) {
-        const int hw = g.hs * g.ws;
-        const int n = P.f_hws.div(rr);
-        const int rem = rr - n * hw;
-        const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
-        const int y0 = ys * g.s - g.p, x0 = xs * g.s - g.p;
-        r_base[i] = ((n * g.hb + y0) * g.wb + x0) * g.cb;
-        for (int kh = 0; kh < g.kh; ++kh)
-          for (int kw = 0; kw < g.kw; ++kw)
-            if ((unsigned)(y0 + kh) < (unsigned)g.hb && (unsigned)(x0 + kw) < (unsigned)g.wb) vm |= 1u << (kh * g.kw + kw);
-      } else if constexpr (OP == OP_SCATTER) {
-        const int hw = cy * cx;
-        const int n = f_cycx.div(rr);
-        const int rem = rr - n * hw;
-        const int ty = f_cx.div(rem), tx = rem - ty * cx;
-        const int y0 = cy0 + ty, x0 = cx0 + tx;  // small pixel of class tap (0, 0)
-        r_base[i] = ((n * g.hs + y0) * g.ws + x0) * g.cs;
-        const int nty = ntx > 0 ? (K / g.cs) / ntx : 0;
-        for (int jy = 0; jy < nty; ++jy)
-          for (int jx = 0; jx < ntx; ++jx)
-            if ((unsigned)(y0 - jy) < (unsigned)g.hs && (unsigned)(x0 - jx) < (unsigned)g.ws) vm |= 1u << (jy * ntx + jx);
-      } else {
-        r_base[i] = rr * P.lda;
-        vm = 1u;
-      }
-      r_vm[i] = ok ? vm : 0u;
-    }
-  }
-
-  auto lf = [&](int kk) -> int {  // DENSE: PyTorch feature index of storage-order k'
-    if (P.a_pix <= 1) return kk;
-    const int pix = P.f_ach.div(kk), c = kk - pix * P.a_ch;
-    return c * P.a_pix + pix;
-  };
-
-  struct Stage {
-    f32x4 a[RA], ay[AY ? RA : 1];
-    f32x4 b[RB], by[BYY ? RB : 1];
-    unsigned am, bm, bone;  // validity masks; bone: WGRAD bias-column slots
-    int ach;                // channel index of the A transform constants
-    int cb0;                // GATHER / SCATTER: channel block of the tile (wave-uniform)
-  };
-
-  // ---------------- global -> registers (every load unconditional)
-  auto fetch = [&](Stage& S, int j) {
-#if defined(CV_ABLATE) && CV_ABLATE == 2
-    j = 0;  // diagnostic build: every tile re-reads the first tile (L1/L2-hot)
-#endif
-    int k0, tap = 0, cb0 = 0;
-    if constexpr (OP == OP_GATHER || OP == OP_SCATTER) {
-      const int cblk = f_ntap.div(j);  // wave-uniform
-      tap = j - cblk * ntap;
-      cb0 = cblk * BK;
-      k0 = tap * CK + cb0;
-    } else {
-      k0 = kbeg + j * BK;
-    }
-    S.cb0 = cb0;
-    S.am = 0;
-    S.bm = 0;
-    S.bone = 0;
-    const float* ax = P.a.x;
-    const float* ayp = P.a.y;
-    if constexpr (ROWS) {
-      const int kq = k0 + 4 * aq;
-      const bool kok = kq < kend;
-      if constexpr (OP == OP_GATHER) {
-        const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
-        const int toff = (kh * g.wb + kw) * g.cb + cb0 + 4 * aq;
-        S.ach = cb0 + 4 * aq;
-#pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          const bool ok = kok && ((r_vm[i] >> tap) & 1u);
-          const int off = ok ? r_base[i] + toff : 0;
-          S.a[i] = g4(ax + off);
-          if constexpr (AY) S.ay[i] = g4(ayp + off);
-          S.am |= (ok ? 1u : 0u) << i;
-        }
-      } else if constexpr (OP == OP_SCATTER) {
-        const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
-        const int toff = cb0 + 4 * aq - (jy * g.ws + jx) * g.cs;
-        S.ach = cb0 + 4 * aq;
-#pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          const bool ok = kok && ((r_vm[i] >> tap) & 1u);
-          const int off = ok ? r_base[i] + toff : 0;
-          S.a[i] = g4(ax + off);
-          if constexpr (AY) S.ay[i] = g4(ayp + off);
-          S.am |= (ok ? 1u : 0u) << i;
-        }
-      } else {  // DENSE, storage-order k'
-        S.ach = bn1d ? kq - kbeg : (P.a_pix > 1 ? P.f_ach.mod(kq) : kq);
-#pragma unroll
-        for (int i = 0; i < RA; ++i) {
-          const bool ok = r_vm[i] && kok;
-          const int off = ok ? r_base[i] + kq : 0;
-          S.a[i] = g4(ax + off);
-          if constexpr (AY) S.ay[i] = g4(ayp + off);
-          S.am |= (ok ? 1u : 0u) << i;
-        }
-      }
-    } else {  // WGRAD A(m = cs, k = small pixel): float4 along cs
-      constexpr int MQ = BM / 4;
-#pragma unroll
-      for (int e = 0; e < RA; ++e) {
-        const int idx = t + NT * e;
-        const int rest = idx >> 2, mq = rest % MQ, kk = 4 * (rest / MQ) + (idx & 3);  // lane quads: 4 k
-        const int pix = k0 + kk, c0 = m0 + 4 * mq;
-        const bool ok = pix < kend && c0 < g.cs;
-        int off = pix * g.cs + c0;
-        off = ok ? off : 0;
-        S.a[e] = g4(ax + off);
-        if constexpr (AY) S.ay[e] = g4(ayp + off);
-        S.am |= (ok ? 1u : 0u) << e;
-      }
-      S.ach = 0;
-    }
-
-    // B
-#pragma unroll
-    for (int e = 0; e < RB; ++e) {
-      const int idx = t + NT * e;
-      if constexpr (BKC) {  // DENSE layout 0: 4 consecutive k of one output column
-        const int n = idx >> 3, kq = k0 + 4 * (idx & 7), col = n0 + n;
-        const bool ok = n < BN && col < N && kq < kend;
-        if constexpr (DBM == DB_KCONT) {
-          int off = col * P.ldb + kq;
-          off = ok ? off : 0;
-          S.b[e] = g4(P.w + off);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int off = col * P.ldb + lf(kq + j);
-            off = ok ? off : 0;
-            S.b[e][j] = P.w[off];
-          }
-        }
-        S.bm |= (ok ? 1u : 0u) << e;
-      } else {
-        constexpr int NQ = BN / 4;
-        int nq, kk;
-        if constexpr (QTB) {  // lane quads: 4 consecutive k of one column quad (quad_transpose staging)
-          const int rest = idx >> 2;
-          nq = rest % NQ;
-          kk = 4 * (rest / NQ) + (idx & 3);
-        } else {  // consecutive lanes: consecutive column quads of one k (coalesced rows, scalar staging)
-          nq = idx % NQ;
-          kk = idx / NQ;
-        }
-        const int col = n0 + 4 * nq, k = k0 + kk;
-        bool ok = kk < BK && k < kend && col < N;
-        int off = 0;
-        if constexpr (OP == OP_GATHER) {
-          off = k0 * g.cs + (kk * g.cs + col);
-        } else if constexpr (OP == OP_SCATTER) {
-          const int jy = f_ntx.div(tap), jx = tap - jy * ntx;
-          const int kh = ry + g.s * jy, kw = rx + g.s * jx;
-          off = ((kh * g.kw + kw) * g.cs + cb0) * g.cb + (kk * g.cb + col);
-        } else if constexpr (OP == OP_DENSE) {
-          off = lf(k) * P.ldb + col;
-        } else {  // WGRAD: B(k = small pixel, col = (tap, cb)) = T(big[gather(pix, tap)][cb])
-          const int hw = g.hs * g.ws;
-          const int nimg = P.f_hws.div(k), rem = k - nimg * hw;
-          const int ys = P.f_ws.div(rem), xs = rem - ys * g.ws;
-          const int nreal = P.N;
-          const int tap = P.f_cb.div(col), c0 = col - tap * g.cb;
-          const int kh = P.f_kw.div(tap), kw = tap - kh * g.kw;
-          const int yb = ys * g.s - g.p + kh, xb = xs * g.s - g.p + kw;
-          if (ok && col == nreal) S.bone |= 1u << e;
-          ok = ok && col < nreal && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
-          off = ((nimg * g.hb + yb) * g.wb + xb) * g.cb + c0;
-        }
-        off = ok ? off : 0;
-        const float* bx_ = (OP == OP_WGRAD) ? P.b.x : P.w;
-        S.b[e] = g4(bx_ + off);
-        if constexpr (BYY) S.by[e] = g4(P.b.y + off);
-        S.bm |= (ok ? 1u : 0u) << e;
-      }
-    }
-  };
-
-  // ---------------- transform + registers -> LDS
-  XC xa, xb;        // register copies of the transform constants
-  int xa_cb0 = -1;  // channel block xa belongs to (GATHER / SCATTER)
-  auto store = [&](Stage& S, int buf) {
-    float* Ab = As + buf * BM * LDK;
-    float* Bb = Bs + buf * BN * LDK;
-    __bf16* Abh = Ah + buf * BM * LDKH;
-    __bf16* Bbh = Bh + buf * BN * LDKH;
-    if constexpr (ROWS) {
-      if constexpr (XA != CV_XF_NONE && OP != OP_DENSE) {
-        if (S.cb0 != xa_cb0) {  // wave-uniform: a new channel block
-          xa = load_xc<XA>(cA, nfa, S.ach);
-          xa_cb0 = S.cb0;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < RA; ++i) {
-        f32x4 v = S.a[i];
-        if constexpr (OP == OP_DENSE) {
-          if constexpr (XA == CV_XF_BNRELU) v = xform4<XA>(v, v, cA, nfa, S.ach);
-          if constexpr (XA == CV_XF_BNBWD) v = xform4<XA>(v, S.ay[i], cA, nfa, S.ach);
-        } else {
-          if constexpr (XA == CV_XF_BNRELU) v = apply_xc<XA>(v, v, xa);
-          if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[i], xa);
-        }
-        if (!((S.am >> i) & 1u)) v = zero4();
-        if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Abh + (ar + 32 * i) * LDKH + 4 * aq) = to_bf16x4(v);
-        else *reinterpret_cast<f32x4*>(Ab + (ar + 32 * i) * LDK + 4 * aq) = v;
-      }
-    } else {
-      constexpr int MQ = BM / 4;
-#pragma unroll
-      for (int e = 0; e < RA; ++e) {
-        const int idx = t + NT * e;
-        const int rest = idx >> 2, mq = rest % MQ, k4 = 4 * (rest / MQ), q = idx & 3;
-        f32x4 v = S.a[e];
-        if constexpr (XA == CV_XF_BNRELU) v = apply_xc<XA>(v, v, xa);
-        if constexpr (XA == CV_XF_BNBWD) v = apply_xc<XA>(v, S.ay[e], xa);
-        if (!((S.am >> e) & 1u)) v = zero4();
-        v = quad_transpose(v, q);  // lane q: row 4mq + q, k = k4 .. k4 + 3
-        if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Abh + (4 * mq + q) * LDKH + k4) = to_bf16x4(v);
-        else *reinterpret_cast<f32x4*>(Ab + (4 * mq + q) * LDK + k4) = v;
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < RB; ++e) {
-      const int idx = t + NT * e;
-      f32x4 v = S.b[e];
-      if constexpr (BKC) {
-        const int n = idx >> 3, kq = idx & 7;
-        if (!((S.bm >> e) & 1u)) v = zero4();
-        if (n < BN) {
-          if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Bbh + n * LDKH + 4 * kq) = to_bf16x4(v);
-          else *reinterpret_cast<f32x4*>(Bb + n * LDK + 4 * kq) = v;
-        }
-      } else {
-        constexpr int NQ = BN / 4;
-        if constexpr (XFB == CV_XF_BNRELU) v = apply_xc<XFB>(v, v, xb);
-        if constexpr (XFB == CV_XF_BNBWD) v = apply_xc<XFB>(v, S.by[e], xb);
-        if (!((S.bm >> e) & 1u)) v = zero4();
-        if (OP == OP_WGRAD && ((S.bone >> e) & 1u)) v = f32x4{1.f, 0.f, 0.f, 0.f};
-        if constexpr (QTB) {
-          const int rest = idx >> 2, nq = rest % NQ, k4 = 4 * (rest / NQ), q = idx & 3;
-          v = quad_transpose(v, q);  // lane q: column 4nq + q, k = k4 .. k4 + 3 (whole quads valid or not)
-          if (k4 < BK) {
-            if constexpr (MT == MMA_BF16) *reinterpret_cast<bf16x4*>(Bbh + (4 * nq + q) * LDKH + k4) = to_bf16x4(v);
-            else *reinterpret_cast<f32x4*>(Bb + (4 * nq + q) * LDK + k4) = v;
-          }
-        } else {
-          const int nq = idx % NQ, kk = idx / NQ;
-          if (kk < BK) {
-            if constexpr (MT == MMA_BF16) {
-              const bf16x4 h = to_bf16x4(v);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) Bbh[(4 * nq + j) * LDKH + kk] = h[j];
-            } else {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) Bb[(4 * nq + j) * LDK + kk] = v[j];
-            }
-          }
-        }
-      }
-    }
-  };
-
-  // ---------------- prologue: first D-1 tiles in flight, then the BN constants
-  Stage stg[D];
-#pragma unroll
-  for (int d = 0; d < D - 1; ++d) fetch(stg[d], max(min(d, nt - 1), 0));
-
-  double* fold_scratch = reinterpret_cast<double*>(As);
-  static_assert(2 * BM * LDK * sizeof(float) >= 4 * NT * sizeof(double) + 16, "fold scratch");
-#if defined(CV_ABLATE) && CV_ABLATE == 3
-  if (false)  // diagnostic build: no constants fold (garbage constants)
-#endif
-  {
-  // every finalised constant set is requested before the first wait (one round trip with the tile loads)
-  SoaPre pa{}, pb{};
-  EpiPre pe{};
-  if constexpr (XA != CV_XF_NONE) {
-    if (!bn1d) pa = soa_issue<XA>(P.a.bn, nfa);
-  }
-  if constexpr (EPI == CV_STAT_BWD) pe = epi_issue(P.ep.ebn, P.ce_n);
-  if constexpr (XA != CV_XF_NONE) {
-    if (bn1d) {
-      const float* src = (XA == CV_XF_BNRELU) ? P.a.bn.cfwd : P.a.bn.cbwd;
-      const int C1 = P.a.bn.C;
-      for (int idx = t; idx < kend - kbeg; idx += NT) {
-        int f = kbeg + idx;
-        if (P.a_pix > 1) {
-          const int pix = f / P.a_ch, c = f - pix * P.a_ch;
-          f = c * P.a_pix + pix;
-        }
-        if (P.a.bn.train && src && P.a.bn.ticket && P.a.bn.ticket[XA == CV_XF_BNRELU ? 0 : 1] != 0u) {
-#pragma unroll
-          for (int q = 0; q < soa_arrays<XA>(); ++q) cA[q * nfa + idx] = src[q * C1 + f];
-        } else if constexpr (XA == CV_XF_BNRELU) {
-          const BnFwdC k = bn_fwd_const(P.a.bn, f);
-          cA[idx] = k.sc;
-          cA[nfa + idx] = k.mu;
-          cA[2 * nfa + idx] = k.be;
-        } else {
-          const BnBwdC k = bn_bwd_const(P.a.bn, f);
-          cA[idx] = k.sc;
-          cA[nfa + idx] = k.c1;
-          cA[2 * nfa + idx] = k.mu;
-          cA[3 * nfa + idx] = k.istd;
-          cA[4 * nfa + idx] = k.c2;
-        }
-      }
-    } else if (!soa_commit<XA>(pa, P.a.bn, nfa, cA)) {
-      fill_soa<XA>(P.a.bn, nfa, cA, fold_scratch);
-    }
-  }
-  if constexpr (XFB != CV_XF_NONE) {  // WGRAD only (long K): issued after A's commit, fewer live registers
-    pb = soa_issue<XFB>(P.b.bn, nfb);
-    if (!soa_commit<XFB>(pb, P.b.bn, nfb, cB)) fill_soa<XFB>(P.b.bn, nfb, cB, fold_scratch);
-  }
-  if constexpr (EPI == CV_STAT_BWD) {
-    BnFwdC* d = reinterpret_cast<BnFwdC*>(cE);
-    const cv_bn& eb = P.ep.ebn;
-    if (!epi_commit(pe, eb, P.ce_n, d)) {
-      bn_fold<NT>(eb, false, fold_scratch, [&](int f, double s, double q, double, double) {
-        if (f < P.ce_n) d[f] = bn_fwd_const_s(eb, f, s, q);
-      });
-    }
-  }
-  }
-  __syncthreads();
-  if constexpr (OP == OP_WGRAD) {  // a thread's channel quads are fixed for the whole K range
-    if constexpr (XA != CV_XF_NONE) {
-      const int c0 = m0 + 4 * ((t >> 2) % (BM / 4));  // (the fetch's lane-quad mapping)
-      xa = load_xc<XA>(cA, nfa, c0 < nfa ? c0 : 0);
-    }
-    if constexpr (XFB != CV_XF_NONE) {
-      const int col = n0 + 4 * ((QTB ? (t >> 2) : t) % (BN / 4));
-      xb = load_xc<XFB>(cB, nfb, col < P.N ? P.f_cb.mod(col) : 0);
-    }
-  }
-  store(stg[0], 0);
-  __syncthreads();
-  CV_STAMP(st1);
-
-  // ---------------- output element offsets; STAT_BWD prefetches the BN inputs at its outputs here,
-  // so their latency hides under the main loop instead of opening the epilogue
-  auto ep_off = [&](int row, int col) -> int {
-    if constexpr (OP == OP_GATHER) {
-      return row * g.cs + col;
-    } else if constexpr (OP == OP_SCATTER) {
-      const int hw = cy * cx;
-      const int nimg = f_cycx.div(row), rem = row - nimg * hw;
-      const int ty = f_cx.div(rem), tx = rem - ty * cx;
-      return ((nimg * g.hb + yb0 + g.s * ty) * g.wb + xb0 + g.s * tx) * g.cb + col;
-    } else {
-      const int oc = (P.o_pix > 1) ? P.f_opix.mod(col) * P.o_ch + P.f_opix.div(col) : col;
-      return row * P.ldo + oc;
-    }
-  };
-  float eyv[EPI == CV_STAT_BWD ? FM : 1][EPI == CV_STAT_BWD ? FN : 1][4];
-  if constexpr (EPI == CV_STAT_BWD && OP != OP_WGRAD) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = n0 + wn * TN + j * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          const bool ok = row < M && col < N;
-          eyv[i][j][r] = P.ep.ey[ok ? ep_off(row, col) : 0];
-        }
-      }
-  }
-
-  // ---------------- main loop: one barrier per K tile, D-1 tiles of loads in flight
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = zero4();
-
-  const int fr = lane & 15, fk = 4 * (lane >> 4);
-  const float* Af = As + (wm * TM + fr) * LDK + fk;
-  const float* Bf = Bs + (wn * TN + fr) * LDK + fk;
-  auto mma = [&](int buf) {
-#if defined(CV_ABLATE) && CV_ABLATE == 1
-    return;  // diagnostic build: no fragment reads / MFMAs
-#endif
-    if constexpr (MT == MMA_BF16) {
-      // lane l: A[row l&15][k = 8(l>>4) .. +7], B[k = 8(l>>4) .. +7][col l&15]; one MFMA per BK=32
-      static_assert(BK == 32, "one 16x16x32 step per K tile");
-      const __bf16* Ab = Ah + buf * BM * LDKH + (wm * TM + fr) * LDKH + 8 * (lane >> 4);
-      const __bf16* Bb = Bh + buf * BN * LDKH + (wn * TN + fr) * LDKH + 8 * (lane >> 4);
-      bf16x8 av[FM], bv[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDKH);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDKH);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-      return;
-    }
-    const float* Ab = Af + buf * BM * LDK;
-    const float* Bb = Bf + buf * BN * LDK;
-    f32x4 av[BK / 16][FM], bv[BK / 16][FN];
-#pragma unroll
-    for (int kc = 0; kc < BK / 16; ++kc) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) av[kc][i] = lds4(Ab + i * 16 * LDK + kc * 16);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bv[kc][j] = lds4(Bb + j * 16 * LDK + kc * 16);
-    }
-#pragma unroll
-    for (int kc = 0; kc < BK / 16; ++kc)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc][i][s], bv[kc][j][s], acc[i][j], 0, 0, 0);
-  };
-  // Steady state: whole groups of D tiles with no exits inside the unrolled group (an exit would
-  // merge control flow and force conservative vmcnt waits); each step fetches tile tt+D-1 (clamped).
-  int tt = 0;
-  for (; tt + D <= nt; tt += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      fetch(stg[(d + D - 1) % D], min(tt + d + D - 1, nt - 1));
-      mma((tt + d) & 1);
-      if (tt + d + 1 < nt) store(stg[(d + 1) % D], (tt + d + 1) & 1);
-      __syncthreads();
-    }
-  }
-  // Tail: the remaining r < D tiles are already staged (slots 0..r-1); no more loads.
-  const int rem = nt - tt;
-#pragma unroll
-  for (int r = 1; r < D; ++r) {
-    if (rem == r) {
-#pragma unroll
-      for (int d = 0; d < r; ++d) {
-        mma((tt + d) & 1);
-        if (d + 1 < r) store(stg[(d + 1) % D], (tt + d + 1) & 1);
-        __syncthreads();
-      }
-    }
-  }
-  CV_STAMP(st2);
-
-  // ---------------- epilogue (same semantics as the generic kernel)
-  constexpr bool STATS = EPI != CV_STAT_NONE;
-  float s1[FN], s2[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    s1[j] = 0.f;
-    s2[j] = 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = n0 + wn * TN + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        float v = acc[i][j][r];
-        if (row >= M || col >= N) continue;
-        if constexpr (OP == OP_WGRAD) {
-          if (P.part) {
-            P.part[((size_t)bz * M + row) * N + col] = v;
-            continue;
-          }
-          const int tap = P.f_cb.div(col), c = col - tap * g.cb;
-          float* dst = (col >= P.N) ? P.gbias + row : P.out + ((size_t)row * g.cb + c) * (g.kh * g.kw) + tap;
-          if (gridDim.z == 1) *dst += v;
-          else atomicAdd(dst, v);
-          continue;
-        } else {
-          const int off = ep_off(row, col);
-          if (P.bias && (!P.accumulate || bz == 0)) v += P.bias[col];
-          if (P.accumulate) {
-            atomicAdd(P.out + off, v);
-            continue;
-          }
-          if constexpr (EPI == CV_STAT_BWD) {
-            const int f = P.f_sdiv.div(col);
-            const float yv = eyv[i][j][r];
-            const BnFwdC k = reinterpret_cast<const BnFwdC*>(cE)[f];
-            if (P.ep.erelu && bn_out(yv, k) <= 0.f) v = 0.f;
-            P.out[off] = v;
-            s1[j] += v;
-            s2[j] += v * ((yv - k.mu) * k.istd);
-          } else {
-            P.out[off] = v;
-            if constexpr (STATS) {
-              s1[j] += v;
-              s2[j] += v * v;
-            }
-          }
-        }
-      }
-    }
-  }
-
-  if constexpr (OP != OP_WGRAD && STATS) {
-    if (!P.accumulate) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        s1[j] += __shfl_xor(s1[j], 16, 64);
-        s1[j] += __shfl_xor(s1[j], 32, 64);
-        s2[j] += __shfl_xor(s2[j], 16, 64);
-        s2[j] += __shfl_xor(s2[j], 32, 64);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int c = wn * TN + j * 16 + lane;
-          red[wm * BN + c] = s1[j];
-          red[WM * BN + wm * BN + c] = s2[j];
-        }
-      }
-      __syncthreads();
-      if (t < BN) {
-        const int col = n0 + t;
-        if (col < N) {
-          double a = 0.0, b = 0.0;
-#pragma unroll
-          for (int w = 0; w < WM; ++w) {
-            a += (double)red[w * BN + t];
-            b += (double)red[WM * BN + w * BN + t];
-          }
-          const int f = P.f_sdiv.div(col);
-          const int C = (EPI == CV_STAT_BWD) ? P.ce_n : P.ep.ebn.C;
-          const int repl = hw_id % CV_STAT_REPL(C);
-          double* so = P.ep.stat_out + (size_t)repl * 2 * C;
-          atomic_add_f64(so + f, a);
-          atomic_add_f64(so + C + f, b);
-        }
-      }
-    }
-    finalize(true);
-  }
+#define CV_TILE_EXIT \
+  do {              \
+    finalize(true); \
+    return;         \
+  } while (0)
+#define CV_TILE_CONSTS_BEGIN {
+#define CV_TILE_CONSTS_END }
+#define CV_TILE_FINALIZE finalize(true)
+#include "cv_gemm_tile.inc"
+#undef CV_TILE_EXIT
+#undef CV_TILE_CONSTS_BEGIN
+#undef CV_TILE_CONSTS_END
+#undef CV_TILE_FINALIZE
 #ifdef CV_STAMPS
   if (t == 0 && g_stamps) {
     const unsigned long long st3 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime();
@@ -913,6 +271,41 @@ void gemm_kernel(const Args P) {
 #endif
 }
 
+// Two tiles per workgroup (GATHER / SCATTER launches with more tiles than one round of resident slots):
+// a 1-D grid of G >= tiles / 2 workgroups, workgroup w takes tiles w and w + G of the tile grid
+// P.tiles_x * P.tiles_y * P.tiles_z.  The BN constants are staged once per workgroup, the last-arriver
+// finalisation runs once per workgroup, and the second round of workgroups — each paying the whole
+// prologue (first-tile burst) and epilogue again — disappears.  The two tiles are two inlined copies of
+// the tile body, not a loop (a loop back-edge kept ~50 more VGPRs live, measured); the narrow tiles ask
+// for 4 resident workgroups so the MNIST backward-data launch (1568 tiles) fits 1024 slots.
+template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
+__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? 4 : (BM == 64 ? CV_FAST_MINW_64 : 1))
+void gemm_kernel2(const Args P) {
+#include "cv_gemm_prelude.inc"
+
+  const int gx = P.tiles_x, gy = P.tiles_y;
+  const int nwg = gx * gy * P.tiles_z;
+  const int hw_id = blockIdx.x;
+  bool first = true;
+  auto tile_body = [&](int tile) {
+    int bx = tile % gx, by = (tile / gx) % gy, bz = tile / (gx * gy);
+#define CV_TILE_EXIT return
+#define CV_TILE_CONSTS_BEGIN \
+  if (first) {               \
+    first = false;
+#define CV_TILE_CONSTS_END }
+#define CV_TILE_FINALIZE ((void)0)
+#include "cv_gemm_tile.inc"
+#undef CV_TILE_EXIT
+#undef CV_TILE_CONSTS_BEGIN
+#undef CV_TILE_CONSTS_END
+#undef CV_TILE_FINALIZE
+  };
+  tile_body(hw_id);
+  if (hw_id + (int)gridDim.x < nwg) tile_body(hw_id + (int)gridDim.x);
+  finalize(true);
+}
+
 #ifndef CV_FAST_DEPTH_BNBWD
 #define CV_FAST_DEPTH_BNBWD 2
 #endif
@@ -922,6 +315,38 @@ void gemm_kernel(const Args P) {
 #ifndef CV_FAST_DEPTH
 #define CV_FAST_DEPTH 2
 #endif
+
+// Resident-workgroup slots of a kernel on the device (occupancy x CUs), cached per (kernel, LDS bytes);
+// 0 disables the two-tile launch (CV_PERSIST=0: one workgroup per tile everywhere, the A/B baseline).
+inline long persist_slots(const void* kern, size_t lds) {
+  static int enabled = -1, cus = 0;
+  if (enabled < 0) {
+    const char* e = getenv("CV_PERSIST");
+    enabled = (e && atoi(e) == 0) ? 0 : 1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+    (void)hipGetLastError();
+  }
+  if (!enabled || cus <= 0) return 0;
+  struct Ent {
+    const void* k;
+    size_t lds;
+    int nb;
+  };
+  static Ent cache[512];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (cache[i].k == kern && cache[i].lds == lds) return (long)cache[i].nb * cus;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    nb = 0;
+  }
+  if (n < 512) cache[n++] = Ent{kern, lds, nb};
+  return (long)nb * cus;
+}
 
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int MT>
 int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
@@ -939,14 +364,18 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
                         : (OP == OP_WGRAD && BM == 128)            ? CV_FAST_DEPTH_WGRAD
                                                                    : CV_FAST_DEPTH;
   auto kern = gemm_kernel<OP, BM, BN, XA, XB, EPI, DEPTH, MT>;
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      cv::set_error("gemm: LDS carve-out of %zu bytes refused: %s", lds, hipGetErrorString(e));
-      return 1;
+  auto carve = [&](const void* k) -> int {
+    if (lds > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        cv::set_error("gemm: LDS carve-out of %zu bytes refused: %s", lds, hipGetErrorString(e));
+        return 1;
+      }
     }
-  }
+    return 0;
+  };
+  if (carve((const void*)kern)) return 1;
   if (g_fast_occ_query) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, NT, lds) != hipSuccess) {
@@ -955,6 +384,24 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
     }
     *g_fast_occ_query = nb;
     return 0;
+  }
+  if constexpr (OP == OP_GATHER || OP == OP_SCATTER) {
+    const long tiles = (long)grid.x * grid.y * grid.z;
+    if (tiles > persist_slots((const void*)kern, lds)) {
+      auto kern2 = gemm_kernel2<OP, BM, BN, XA, XB, EPI, DEPTH, MT>;
+      const long slots = persist_slots((const void*)kern2, lds);
+      if (slots > 0) {
+        if (carve((const void*)kern2)) return 1;
+        Args p = a;
+        p.tiles_x = (int)grid.x;
+        p.tiles_y = (int)grid.y;
+        p.tiles_z = (int)grid.z;
+        const long G = slots > (tiles + 1) / 2 ? slots : (tiles + 1) / 2;  // every tile is w or w + G
+        hipLaunchKernelGGL(kern2, dim3((unsigned)G), dim3(NT), lds, st, p);
+        CV_LAUNCH_CHECK("gemm2");
+        return 0;
+      }
+    }
   }
   hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
   CV_LAUNCH_CHECK("gemm");

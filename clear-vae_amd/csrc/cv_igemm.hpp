@@ -47,6 +47,7 @@ struct Args {
   int ldo, o_pix, o_ch;      // DENSE: out row stride; permutation of output columns
   int ca_n, cb_n, ce_n;      // feature counts of a / b / epilogue BN constants (0 = unused)
   int mma;                   // CV_MMA_FP32 / CV_MMA_BF16 operand precision of the specialised core
+  int tiles_x, tiles_y, tiles_z;  // two-tile launch of the specialised core (gemm_kernel2): the tile grid
   // fast divisors (filled by finalize_divs at launch)
   FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
 };
