@@ -289,6 +289,10 @@ void gemm_kernel2(const Args P) {
   bool first = true;
   auto tile_body = [&](int tile) {
     int bx = tile % gx, by = (tile / gx) % gy, bz = tile / (gx * gy);
+    // thread indices re-derived per tile (shadowing the prelude's): the captured copies cost 5 VGPRs of
+    // spills on the BN-backward narrow tiles
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int wm = wid / WN, wn = wid % WN;
 #define CV_TILE_EXIT return
 #define CV_TILE_CONSTS_BEGIN \
   if (first) {               \
