@@ -237,8 +237,10 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
 #endif
 // MT: MMA_F32 (v_mfma_f32_16x16x4_f32, fp32 operands) or MMA_BF16 (operands rounded to bf16 when
 // staged into LDS after the fp32 transform, v_mfma_f32_16x16x32_bf16, fp32 accumulation)
+// (the deep-ring instances, D >= 4, serve under-filled launches only: 2 resident workgroups suffice there)
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
-__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? CV_FAST_MINW_SMALL : (BM == 64 ? CV_FAST_MINW_64 : 1))
+__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? (D >= 4 ? 2 : CV_FAST_MINW_SMALL)
+                                                        : (BM == 64 ? CV_FAST_MINW_64 : 1))
 void gemm_kernel(const Args P) {
 #include "cv_gemm_prelude.inc"
 
@@ -321,19 +323,25 @@ void gemm_kernel2(const Args P) {
 #endif
 
 // Resident-workgroup slots of a kernel on the device (occupancy x CUs), cached per (kernel, LDS bytes);
-// 0 disables the two-tile launch (CV_PERSIST=0: one workgroup per tile everywhere, the A/B baseline).
-inline long persist_slots(const void* kern, size_t lds) {
-  static int enabled = -1, cus = 0;
-  if (enabled < 0) {
+// 0 when unknown.
+inline bool persist_enabled() {  // CV_PERSIST=0: no two-tile launch (one workgroup per tile), the A/B baseline
+  static int on = -1;
+  if (on < 0) {
     const char* e = getenv("CV_PERSIST");
-    enabled = (e && atoi(e) == 0) ? 0 : 1;
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on != 0;
+}
+inline long resident_slots(const void* kern, size_t lds) {
+  static int cus = -1;
+  if (cus < 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 0;
     (void)hipGetLastError();
   }
-  if (!enabled || cus <= 0) return 0;
+  if (cus <= 0) return 0;
   struct Ent {
     const void* k;
     size_t lds;
@@ -351,6 +359,22 @@ inline long persist_slots(const void* kern, size_t lds) {
   if (n < 512) cache[n++] = Ent{kern, lds, nb};
   return (long)nb * cus;
 }
+
+// Deep operand ring for under-filled launches (CV_DEEP=0: off, the A/B baseline): a GATHER / SCATTER launch
+// whose workgroups fill less than half of one round of resident slots leaves ~1-2 workgroups per CU, so
+// nothing hides the K loop's load latency but the register ring itself; those launches take a 4-deep ring
+// (3 K tiles in flight), which costs registers the under-filled launch does not need for occupancy.
+inline bool deep_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CV_DEEP");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on != 0;
+}
+#ifndef CV_FAST_DEPTH_DEEP
+#define CV_FAST_DEPTH_DEEP 4
+#endif
 
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int MT>
 int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
@@ -389,11 +413,22 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
     *g_fast_occ_query = nb;
     return 0;
   }
+  if constexpr ((OP == OP_GATHER || OP == OP_SCATTER) && MT == MMA_F32 && DEPTH < CV_FAST_DEPTH_DEEP) {
+    const long tiles = (long)grid.x * grid.y * grid.z;
+    const long slots1 = deep_enabled() ? resident_slots((const void*)kern, lds) : 0;
+    if (slots1 > 0 && 2 * tiles <= slots1) {
+      auto kern4 = gemm_kernel<OP, BM, BN, XA, XB, EPI, CV_FAST_DEPTH_DEEP, MT>;
+      if (carve((const void*)kern4)) return 1;
+      hipLaunchKernelGGL(kern4, grid, dim3(NT), lds, st, a);
+      CV_LAUNCH_CHECK("gemm_deep");
+      return 0;
+    }
+  }
   if constexpr (OP == OP_GATHER || OP == OP_SCATTER) {
     const long tiles = (long)grid.x * grid.y * grid.z;
-    if (tiles > persist_slots((const void*)kern, lds)) {
+    if (persist_enabled() && tiles > resident_slots((const void*)kern, lds)) {
       auto kern2 = gemm_kernel2<OP, BM, BN, XA, XB, EPI, DEPTH, MT>;
-      const long slots = persist_slots((const void*)kern2, lds);
+      const long slots = resident_slots((const void*)kern2, lds);
       if (slots > 0) {
         if (carve((const void*)kern2)) return 1;
         Args p = a;
