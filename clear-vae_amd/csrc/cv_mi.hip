@@ -134,7 +134,10 @@ __device__ __forceinline__ float mlp_bwd_row(const MlpLds<DM>& L, int dx, int h,
 
 // ---------------------------------------------------------------- workspace
 constexpr int MI_MAXN = 4096;
-constexpr int MI_NB = 32;                  // max row workgroups whose partials are folded
+#ifndef CV_MI_NB
+#define CV_MI_NB 64  // (64 row workgroups for the learning step measured +0.2 % on C3 over 32)
+#endif
+constexpr int MI_NB = CV_MI_NB;            // max row workgroups whose partials are folded
 constexpr int MI_FP = 2 + 128;             // per-workgroup forward partial: acc0, acc1, E[64], M[64]
 constexpr int MI_GSZ = 4 * 64 * 64 + 256;  // per-workgroup learning-gradient partial (lane-major)
 struct MiWork {
