@@ -19,17 +19,18 @@ struct RunArgs {
   float momentum;
 };
 
-// one block per layer; replica folds spread over the block for narrow layers
+// blockIdx.y = layer.  Narrow layers (C < 256): one block, replica folds spread over the block (bn_fold);
+// wide layers: blockIdx.x takes channels [256 x, 256 x + 256), one channel per thread (the BN1d layer's
+// 2048 features were 8 sequential replica folds per thread in one block)
 __global__ __launch_bounds__(256) void bn_running_kernel(const RunArgs a) {
   __shared__ double scratch[4 * 256];
   const int l = blockIdx.y;
   if (l >= a.nl) return;
   const cv_bn& b = a.bn[l];
-  if (threadIdx.x == 0 && a.nbt[l]) a.nbt[l][0] += 1;
   float* rm = const_cast<float*>(b.running_mean);
   float* rv = const_cast<float*>(b.running_var);
   const float m = a.momentum;
-  bn_fold<256>(b, false, scratch, [&](int c, double s, double q, double, double) {
+  auto update = [&](int c, double s, double q, double, double) {
     const double n = (double)b.count;
     const double mean = s / n;
     double var = q / n - mean * mean;
@@ -37,7 +38,19 @@ __global__ __launch_bounds__(256) void bn_running_kernel(const RunArgs a) {
     const double unbiased = (b.count > 1) ? var * n / (n - 1.0) : var;
     rm[c] = m * (float)mean + (1.0f - m) * rm[c];
     rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
-  });
+  };
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.nbt[l]) a.nbt[l][0] += 1;
+  if (b.C >= 256) {  // (the same per-channel fold as bn_fold's one-channel-per-thread path)
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < b.C) {
+      double s = 0.0, q = 0.0;
+      bn_sums(b.stat, b.C, c, s, q);
+      update(c, s, q, 0.0, 0.0);
+    }
+    return;
+  }
+  if (blockIdx.x != 0) return;
+  bn_fold<256>(b, false, scratch, update);
 }
 
 struct GradArgs {
@@ -770,7 +783,7 @@ extern "C" int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum
   }
   a.nl = nlayers;
   a.momentum = momentum;
-  hipLaunchKernelGGL(bn_running_kernel, dim3(1, nlayers), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(bn_running_kernel, dim3(cdiv(cmax, 256), nlayers), dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("bn_update_running");
   return 0;
 }
