@@ -487,6 +487,7 @@ struct StepRedArgs {
   float* db[MAX_BN];
   int64_t* nbt[MAX_BN];
   int nbn, grads, running;
+  int bnblk0[MAX_BN + 1];  // prefix sums of the blocks of each BN layer (wide layers: 256 channels per block)
   float momentum;
   // fused Adam (cv_step_reduce_adam; ap == nullptr: off).  Every gradient this launch finalises is stepped
   // where it is produced; the rest of the arena lies in the plain ranges [plain0, plain0 + plainn), stepped
@@ -605,9 +606,9 @@ __device__ __forceinline__ void step_reduce_body(const StepRedArgs& a, const Ada
     for (int sgm = b; sgm < a.blk0[a.nd]; sgm += a.nprod) defer_segment(a, ac, adam, sgm, t, red);
     return;
   }
-  const int l = b - a.nprod;
-  if (l >= a.nbn) {  // fused Adam over a plain range of the arena
-    const int pb = l - a.nbn;
+  const int lb = b - a.nprod;
+  if (lb >= a.bnblk0[a.nbn]) {  // fused Adam over a plain range of the arena
+    const int pb = lb - a.bnblk0[a.nbn];
     if (!adam || pb >= a.pblk0[a.nplain]) return;
     int r = 0;
     while (r + 1 < a.nplain && pb >= a.pblk0[r + 1]) ++r;
@@ -616,7 +617,44 @@ __device__ __forceinline__ void step_reduce_body(const StepRedArgs& a, const Ada
     for (long i = i0 + t; i < i1; i += 256) adam_elem(a, ac, i, a.ag[i]);
     return;
   }
+  int l = 0;
+  while (l + 1 < a.nbn && lb >= a.bnblk0[l + 1]) ++l;
+  const int chunk = lb - a.bnblk0[l];
   const cv_bn& bn = a.bn[l];
+  if (bn.C >= 256) {  // wide layers (the BN1d's 2048 features): one channel per thread, 256 channels per block,
+    // the same per-channel replica folds as bn_fold's one-channel-per-thread path
+    const int c = chunk * 256 + t;
+    if (a.running && t == 0 && chunk == 0 && a.nbt[l]) a.nbt[l][0] += 1;
+    if (c >= bn.C) return;
+    if (a.grads) {
+      double s1 = 0.0, s2 = 0.0;
+      if (bn.train) bn_sums(bn.gstat, bn.C, c, s1, s2);
+      float* dg = a.dg[l];
+      float* db = a.db[l];
+      if (db) {
+        db[c] = (float)s1;
+        if (adam) adam_elem(a, ac, db + c - a.ag, (float)s1);
+      }
+      if (dg) {
+        dg[c] = (float)s2;
+        if (adam) adam_elem(a, ac, dg + c - a.ag, (float)s2);
+      }
+    }
+    if (a.running) {
+      double s1 = 0.0, q = 0.0;
+      if (bn.train) bn_sums(bn.stat, bn.C, c, s1, q);
+      const double n = (double)bn.count;
+      const double mean = s1 / n;
+      double var = q / n - mean * mean;
+      if (var < 0.0) var = 0.0;
+      const double unbiased = (bn.count > 1) ? var * n / (n - 1.0) : var;
+      float* rm = const_cast<float*>(bn.running_mean);
+      float* rv = const_cast<float*>(bn.running_var);
+      rm[c] = a.momentum * (float)mean + (1.0f - a.momentum) * rm[c];
+      rv[c] = a.momentum * (float)unbiased + (1.0f - a.momentum) * rv[c];
+    }
+    return;
+  }
   if (a.grads) {  // dgamma = sum dz*xhat, dbeta = sum dz (the backward sums)
     cv_bn gb = bn;
     gb.stat = bn.gstat;
@@ -958,13 +996,14 @@ static int step_reduce_launch(const cv_wgrad_defer* defers, int ndefer, const cv
     a.nbt[i] = nbt ? nbt[i] : nullptr;
   }
   a.nbn = nbn;
+  for (int i = 0; i < nbn; ++i) a.bnblk0[i + 1] = a.bnblk0[i] + (bn[i].C >= 256 ? cdiv(bn[i].C, 256) : 1);
   a.grads = (dgamma || dbeta) ? 1 : 0;
   a.running = running;
   a.momentum = momentum;
   // without Adam every segment has its own block (no arrival ticket); with it the segments are shared by at most
   // 2048 blocks so the ticket stays cheap
   a.nprod = adam_arena ? (nb < 2048 ? nb : 2048) : nb;
-  int blocks = a.nprod + nbn;
+  int blocks = a.nprod + a.bnblk0[nbn];
   if (adam_arena) {
     // the gradient ranges this launch finalises (steps them itself); the complement is stepped by plain blocks
     const float* g0 = adam_arena[1];
