@@ -280,6 +280,17 @@ def roofline_of(config, G, instep, precision, engine=None):
                 roof["traffic"] = round(float(t["traffic_bytes"]))
         except (OSError, ValueError, KeyError):
             pass
+    # MFMA utilisation of the same call from the committed counter pass (profiles/pmc_mfma.py), when taken
+    upath = os.path.join(ROOT, "profiles", "mfma_util.jsonl")
+    if os.path.exists(upath):
+        try:
+            key = f"{config} {label.split(':', 1)[0]}"
+            for line in open(upath):
+                u = json.loads(line).get(key)
+                if u is not None:
+                    roof["mfma_util_pmc"] = round(float(u["mfma_util_median"]), 4)
+        except (OSError, ValueError, KeyError):
+            pass
     return roof
 
 
