@@ -8,8 +8,13 @@ code/run_styledmnist_downstream_expr.py:231-238), fp32, one fused HIP training s
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config mnist|celeba-mim|celeba|camelyon-bf16]
 
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL): per-GPU batch fixed
-(weak scaling); value = images processed by all ranks / max-over-ranks wall time.
+--gpus N > 1: one process per GPU over RCCL.  Run directly, bench.py starts `torch.distributed.run
+--nproc-per-node N` as a child process (before any GPU call) and passes its exit status on; under an
+external torch.distributed.run WORLD_SIZE must equal N.  Per-GPU batch fixed (weak scaling); value = images
+processed by all ranks / max-over-ranks wall time.  CV_DIST_BACKEND=gloo rehearses the flow with all ranks on
+one GPU.  The default config also times, at every N, the weak-scaling keys "celeba" (VAE64 CLEAR-VAE fp32,
+256 per GPU: north_star's scaling target), "pacs" (32 per GPU: configs[3] at N=4) and "camelyon_bf16" (128
+per GPU bf16: configs[4] at N=8), each with the exposed all-reduce time per step at N > 1.
 
 After the timed region (nothing below is inside it):
   (1) an in-step pass: the step's programs are enqueued eagerly behind a spin kernel long enough for the
@@ -21,9 +26,9 @@ After the timed region (nothing below is inside it):
       torch-CPU) on a bounded sample, and the ELBO (and, for CLEAR-MIM, MI) error of one HIP step against
       the fp64 CPU reference on the same batch / weights / noise;
   (3) default config at N=1: configs[2] (CelebA 64x64 bs=256 CLEAR-MIM CLUB-S) is timed the same way
-      and reported under "c3"; the per-GPU shards of configs[3] (PACS, VAE64 bs=32 fp32) and configs[4]
-      (Camelyon17, VAE64 bs=128 bf16) are timed on this one GPU under "c4_per_gpu" / "c5_per_gpu"
-      (img/s of one rank; their DDP totals are the driver's multi-GPU runs);
+      and reported under "c3" with its own CPU baseline; the weak-scaling keys above at N=1 carry the
+      in-step roofline of their dominant call ("c4_per_gpu" / "c5_per_gpu" repeat "pacs" /
+      "camelyon_bf16", the round-2 names);
   (4) default / camelyon-bf16 config at N=1: the device input pipeline (Resize((64, 64)) + ToTensor of a
       96x96x3 uint8 batch of 1024, cv_load_batch_u8) under "input_pipeline", with Pillow's own transform
       timed beside it on one host core.
@@ -96,13 +101,31 @@ def layer_flops(spec):
 
 
 def step_flops_per_image(spec, mode):
-    """training = 3x forward; CLEAR-MIM adds 5 forward-only passes."""
+    """training = 3x forward; CLEAR-MIM adds 5 forward-only passes (the reference's work)."""
     f = layer_flops(spec)
     return 3 * f + (5 * f if mode == "mim" else 0)
 
 
+def encoder_flops(spec):
+    """Forward FLOPs per image of the encoder convs and the 4 heads."""
+    f = 0
+    for c in spec.enc:
+        f += 2 * c.h_out * c.w_out * c.c_out * c.c_in * c.mod.kernel_size[0] * c.mod.kernel_size[1]
+    return f + 2 * spec.F * 4 * spec.d
+
+
+def executed_flops_per_image(spec, mode):
+    """FLOPs the fused step executes per image: CLEAR-MIM's 5 estimator-update forwards share one encoder pass
+    (same batch, same post-Adam weights: cvhip/engine.py make_learn), so 4 encoder passes are not run."""
+    f = step_flops_per_image(spec, mode)
+    return f - (4 * encoder_flops(spec) if mode == "mim" else 0)
+
+
 def _programs(G):
-    progs = [("fwd", G["fwd"]), ("dec", G["dec"]), ("lat", G["lat"]), ("enc", G["enc"]), ("upd", G["upd"])]
+    progs = [("fwd", G["fwd"]), ("dec", G["dec"]), ("lat", G["lat"]), ("enc", G["enc"])]
+    if G.get("enc2") is not None:  # data parallel: the shallow-encoder bucket's program
+        progs.append(("enc2", G["enc2"]))
+    progs.append(("upd", G["upd"]))
     learn = G.get("learn")
     if isinstance(learn, list):  # data-parallel CLEAR-MIM: (gradient, Adam) program pairs
         for j, (gp, ap) in enumerate(learn):
@@ -306,28 +329,41 @@ def cpu_model():
 
 def cpu_baseline(cfg, budget_s=15.0):
     """The reference's training loop composition on the host cores (oracle/ref_loop.py, torch-CPU fp32),
-    on a bounded sample of the same workload."""
+    on a bounded sample of the same workload.  The host cores of the GPU boxes are shared, so single steps
+    vary run to run: the value is the batch over the MEDIAN step time of the sample (mean and spread
+    reported beside it), with the threads and the CPU affinity used."""
+    import statistics
+
     from oracle.ref_loop import RefLoop
 
     arch, z, C, hw, B, mode, nl, hp, est = cfg
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):  # pragma: no cover
+        affinity = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", affinity))
     torch.set_num_threads(threads)
     loop = RefLoop(arch, z, C, mode, dict(hp))
     g = torch.Generator().manual_seed(1000)
     data = [(torch.rand(B, C, hw, hw, generator=g), torch.randint(0, nl, (B,), generator=g)) for _ in range(4)]
     loop.step(*data[0])  # warm-up (allocator, oneDNN primitives)
-    steps, work = 0, 0.0
-    while work < budget_s and steps < 400:
-        X, y = data[steps % len(data)]
+    times = []
+    while sum(times) < budget_s and len(times) < 400:
+        X, y = data[len(times) % len(data)]
         t0 = time.perf_counter()
         loop.step(X, y)
-        work += time.perf_counter() - t0
-        steps += 1
-    return {"value": round(B * steps / work, 1), "unit": "images/s", "cores": torch.get_num_threads(),
-            "cpu_model": cpu_model(), "kind": "port",
-            "sample": f"{steps} steps x bs={B} {arch} {'CLEAR-VAE' if mode == 'clear' else 'CLEAR-MIM CLUB-S'} fp32: "
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    kind = "CLEAR-VAE" if mode == "clear" else "CLEAR-MIM CLUB-S"
+    return {"value": round(B / med, 1), "unit": "images/s", "cores": torch.get_num_threads(),
+            "cpu_affinity": affinity, "cpu_model": cpu_model(), "kind": "port",
+            "mean_value": round(B * len(times) / sum(times), 1),
+            "step_ms_p10_p50_p90": [round(1e3 * statistics.quantiles(times, n=10)[0], 2) if len(times) > 1 else None,
+                                    round(1e3 * med, 2),
+                                    round(1e3 * statistics.quantiles(times, n=10)[-1], 2) if len(times) > 1 else None],
+            "sample": f"{len(times)} steps x bs={B} {arch} {kind} fp32 (median step): "
                       "oracle/ref_loop.py, the reference's module/loss/trainer step composition on torch-CPU "
-                      "(within 1% of the reference's own CLEARVAETrainer._train in the dev container, DESIGN 7)"}
+                      "(within 1% of the reference's own _train in the dev container, DESIGN 7)"}
 
 
 def step_error(cfg, device):
@@ -421,7 +457,10 @@ def run_workload(name, cfg, steps, warmup, device, world, rank, detail=True, ker
     eng.sync_host_state()
     value = world * B * steps / max(el, 1e-12)
     res = {"value": value, "el": el, "ms_per_step": el / max(steps, 1) * 1e3, "finite": finite, "eng": eng,
-           "algorithmic_tflops": step_flops_per_image(eng.spec, mode) * value / 1e12}
+           "algorithmic_tflops": step_flops_per_image(eng.spec, mode) * value / 1e12,
+           "executed_tflops": executed_flops_per_image(eng.spec, mode) * value / 1e12}
+    if world > 1:
+        res["comm"] = comm_pass(eng, step, warmup + steps, device)
     if detail:
         G = eng.graphs[B]
         instep = instep_pass(eng, G)
@@ -438,6 +477,30 @@ def run_workload(name, cfg, steps, warmup, device, world, rank, detail=True, ker
                              f"{fl / (ms * 1e-3) / 1e12:12.2f}\n")
                 fh.write(f"{'total (sum of calls)':60s} {sum(instep.values()):11.4f} {sum(iso.values()):9.4f}\n")
     return res
+
+
+def comm_pass(eng, step, i0, device, k=10):
+    """Data parallel: the exposed (not overlapped) gradient all-reduce time per step, from HIP events around
+    every wait for the buckets on the step's stream over K instrumented steps (after the timed region), max
+    over ranks; with the bucket sizes."""
+    eng.comm_probe = []
+    torch.cuda.synchronize()
+    for i in range(k):
+        step(i0 + i)
+    torch.cuda.synchronize()
+    tot = {"vae": 0.0, "est": 0.0}
+    for kind, e0, e1 in eng.comm_probe:
+        tot[kind] += e0.elapsed_time(e1)
+    eng.comm_probe = None
+    t = torch.tensor([tot["vae"] / k, tot["est"] / k], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {"exposed_allreduce_ms": round(float(t[0]), 4),
+           "bucket_bytes": [4 * (hi - lo) for lo, hi in eng.buckets.bounds],
+           "timing": "HIP events around the wait for the gradient buckets on the step stream, mean of "
+                     f"{k} steps, max over ranks"}
+    if eng.two_nets:
+        out["exposed_estimator_allreduce_ms"] = round(float(t[1]), 4)
+    return out
 
 
 def pipeline_pass(device, n=1024, hw=96, out=64, reps=50, cpu_budget_s=3.0):
@@ -504,6 +567,37 @@ def workload_label(name, cfg, world):
             "model": arch, "global_batch": world * B, "seq_len": None, "parallelism": f"dp{world}"}
 
 
+def spawn_ranks(n):
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# weak-scaling workloads timed at every N by the default run (per-GPU batch fixed): north_star's 75 % scaling
+# target is on CelebA 64x64 (code/run_celeba_downstream_expr.py:225-234, VAE64 z=64 CLEAR-VAE, 256 per GPU);
+# PACS 32 per GPU is configs[3] at N=4, Camelyon17 128 per GPU bf16 is configs[4] at N=8
+SCALING_KEYS = (("celeba", "celeba", 256), ("pacs", "pacs", 32), ("camelyon_bf16", "camelyon-bf16", 128))
+
+
+def scaling_entry(cname, cfg, steps, device, world, rank, detail):
+    r = run_workload(cname, cfg, steps, 10, device, world, rank, detail=detail)
+    e = {"value": round(r["value"], 1), "unit": "images/s", "n_gpus": world, "scaling": "weak",
+         "per_gpu_batch": cfg[4], "global_batch": world * cfg[4], "ms_per_step": round(r["ms_per_step"], 4),
+         "steps": steps, "dtype": cfg[7].get("precision", "fp32"), "config": workload_label(cname, cfg, world),
+         "losses_finite": r["finite"], "algorithmic_tflops": round(r["algorithmic_tflops"], 3)}
+    if "comm" in r:
+        e.update(r["comm"])
+    if r.get("roofline") is not None:
+        e["roofline"] = r["roofline"]
+    return e
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -519,11 +613,34 @@ def main():
                     help="profiling mode: after warmup, launch this step-program call (e.g. 'enc[4]') --reps "
                          "times back to back and exit (for rocprofv3 --pmc)")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check without a GPU: the ranks join a gloo group and rank 0 prints the world")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start torch.distributed.run as a child process before anything touches the GPU
+        # (this process never initialises HIP) and pass its exit status on; rank 0 prints the line
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (torch.distributed.run --nproc-per-node "
+                 "must equal --gpus)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:  # (tests/test_bench_launch.py: the rank launch on a machine without a GPU)
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            world_seen = int(t.item())
+        else:
+            world_seen = 1
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "world_seen": world_seen, "gpus_arg": args.gpus}),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # RCCL over xGMI; CV_DIST_BACKEND=gloo rehearses the multi-rank flow with several ranks on one GPU
     backend = os.environ.get("CV_DIST_BACKEND", "nccl")
     if world > 1 and backend != "nccl":
@@ -559,23 +676,28 @@ def main():
     res = run_workload(args.config, cfg, args.steps, args.warmup, device, world, rank,
                        detail=not args.no_kernel_pass, kernel_table=args.kernel_table)
     c3 = None
-    if args.config == "mnist" and world == 1 and not args.no_c3 and args.batch is None:
+    extra = args.config == "mnist" and not args.no_c3 and args.batch is None
+    if extra and world == 1:
         ccfg = CONFIGS["celeba-mim"]
         k3 = min(args.steps, 60)
         r3 = run_workload("celeba-mim", ccfg, k3, 5, device, 1, 0, detail=not args.no_kernel_pass)
         c3 = {"metric": "training images/sec (configs[2])", "value": round(r3["value"], 1), "unit": "images/s",
               "ms_per_step": round(r3["ms_per_step"], 4), "steps": k3, "warmup": 5, "dtype": "fp32",
               "config": workload_label("celeba-mim", ccfg, 1),
-              "algorithmic_tflops": round(r3["algorithmic_tflops"], 3), "losses_finite": r3["finite"],
-              "roofline": r3.get("roofline")}
-        shards = {}
-        for key, cname in (("c4_per_gpu", "pacs"), ("c5_per_gpu", "camelyon-bf16")):
+              "algorithmic_tflops": round(r3["algorithmic_tflops"], 3),
+              "algorithmic_tflops_note": "the reference's work (6 VAE forwards per step, SURVEY 8d)",
+              "executed_tflops": round(r3["executed_tflops"], 3),
+              "executed_tflops_note": "the work run: the 5 estimator-update forwards share one encoder pass",
+              "losses_finite": r3["finite"], "roofline": r3.get("roofline")}
+    # the weak-scaling keys at every N (per-GPU batch fixed; at N=1 the same workloads on one GPU, with the
+    # in-step roofline of their dominant call)
+    scaling = {}
+    if extra:
+        for key, cname, bs in SCALING_KEYS:
             ccfg = CONFIGS[cname]
-            r = run_workload(cname, ccfg, min(args.steps, 100), 10, device, 1, 0, detail=False)
-            shards[key] = {"value": round(r["value"], 1), "unit": "images/s", "ms_per_step": round(r["ms_per_step"], 4),
-                           "steps": min(args.steps, 100), "dtype": ccfg[7].get("precision", "fp32"),
-                           "config": workload_label(cname, ccfg, 1), "losses_finite": r["finite"],
-                           "algorithmic_tflops": round(r["algorithmic_tflops"], 3)}
+            assert ccfg[4] == bs, (cname, ccfg[4])
+            scaling[key] = scaling_entry(cname, ccfg, min(args.steps, 100), device, world, rank,
+                                         detail=(world == 1 and not args.no_kernel_pass))
     if rank == 0:
         rec = {
             "metric": "training images/sec at bs=512; ELBO rel-err vs CPU ref",
@@ -596,6 +718,12 @@ def main():
             "roofline": res.get("roofline"),
             "instep_sum_ms": round(res["instep_sum_ms"], 4) if "instep_sum_ms" in res else None,
         }
+        if "comm" in res:
+            rec.update(res["comm"])
+        rec.update(scaling)
+        if world == 1 and scaling:  # (the round-2 names of the configs[3] / configs[4] per-GPU shards)
+            rec["c4_per_gpu"] = scaling["pacs"]
+            rec["c5_per_gpu"] = scaling["camelyon_bf16"]
         if world == 1:
             try:
                 rec.update(step_error(cfg, device))
@@ -606,8 +734,12 @@ def main():
                     c3.update(step_error(CONFIGS["celeba-mim"], device))
                 except Exception as e:  # pragma: no cover
                     c3["elbo_rel_err"] = repr(e)
+                if not args.no_cpu_baseline:
+                    try:
+                        c3["cpu_baseline"] = cpu_baseline(CONFIGS["celeba-mim"], budget_s=12.0)
+                    except Exception as e:  # pragma: no cover
+                        c3["cpu_baseline"] = {"error": repr(e)}
                 rec["c3"] = c3
-                rec.update(shards)
             if args.config in ("mnist", "camelyon-bf16") and args.batch is None:
                 try:
                     rec["input_pipeline"] = pipeline_pass(device)

@@ -307,7 +307,9 @@ void gemm_kernel2(const Args P) {
 #undef CV_TILE_CONSTS_END
 #undef CV_TILE_FINALIZE
   };
-  tile_body(hw_id);
+  // the host clamps the grid to at most `tiles` workgroups; the guard keeps a workgroup without a tile
+  // (a grid larger than the tile count) from decoding a bogus tile (a parity class bz >= tiles_z)
+  if (hw_id < nwg) tile_body(hw_id);
   if (hw_id + (int)gridDim.x < nwg) tile_body(hw_id + (int)gridDim.x);
   finalize(true);
 }
@@ -435,7 +437,10 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
         p.tiles_x = (int)grid.x;
         p.tiles_y = (int)grid.y;
         p.tiles_z = (int)grid.z;
-        const long G = slots > (tiles + 1) / 2 ? slots : (tiles + 1) / 2;  // every tile is w or w + G
+        // every tile is w or w + G, and no workgroup is without a first tile (G <= tiles): the two-tile
+        // entry asks for more resident workgroups than the one-tile one, so slots can exceed tiles here
+        long G = slots > (tiles + 1) / 2 ? slots : (tiles + 1) / 2;
+        if (G > tiles) G = tiles;
         hipLaunchKernelGGL(kern2, dim3((unsigned)G), dim3(NT), lds, st, p);
         CV_LAUNCH_CHECK("gemm2");
         return 0;

@@ -80,9 +80,14 @@ class ResizePlan:
 
 
 def load_batch(images: torch.Tensor, index: torch.Tensor | None, out_hw, labels=None, styles=None, out=None,
-               stream=None):
+               stream=None, checked: bool = True):
     """Resize + ToTensor of images[index] (uint8 [N, H, W] or [N, H, W, C] on the device) into fp32
-    [n, C, out_h, out_w]; returns (X, labels[index] or None, styles[index] or None)."""
+    [n, C, out_h, out_w]; returns (X, labels[index] or None, styles[index] or None).
+
+    The kernel addresses images / labels / styles through `index` without bounds checks, so a caller's
+    index is range-checked on the host first (IndexError, as tensor indexing would raise; one device
+    read).  checked=False skips that for indices the caller made in range itself (DeviceLoader's own
+    permutation)."""
     if images.device.type != "cuda" or images.dtype != torch.uint8:
         raise RuntimeError("clear-vae_amd: load_batch needs a uint8 image tensor on the ROCm device")
     imgs = images if images.dim() == 4 else images.unsqueeze(-1)
@@ -95,6 +100,10 @@ def load_batch(images: torch.Tensor, index: torch.Tensor | None, out_hw, labels=
     if index is not None:
         idx = index.to(device=images.device, dtype=torch.int64).contiguous()
         n = idx.numel()
+        if checked and n:
+            lo, hi = (int(v) for v in torch.aminmax(idx))
+            if lo < 0 or hi >= N:
+                raise IndexError(f"load_batch: index out of range [{lo}, {hi}] for {N} images")
     plan = ResizePlan.get(H, W, oh, ow, C, images.device)
     if out is None:
         out = torch.empty(n, C, oh, ow, dtype=torch.float32, device=images.device)

@@ -197,6 +197,8 @@ class ClearStep:
         # steps) all advance one stream instead of replaying the same noise from 0
         self.seed, self.offset = rng.offset_tensor(self.device)
         self.world = _dist_world()
+        if self.world > 1:  # a noise stream per rank (the shards are different samples; equal noise would tie them)
+            self.seed = (self.seed ^ (0x9E3779B97F4A7C15 * cvdist.rank())) & 0xFFFFFFFFFFFFFFFF
         self.gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
         self.graphs = {}  # n -> dict
         self.graphs_enabled = True
@@ -217,8 +219,7 @@ class ClearStep:
             cvdist.broadcast_flat(self.arena.flat)
             if self.two_nets:
                 cvdist.broadcast_flat(self.est_arena.flat)
-            split = self._bucket_split()
-            self.buckets = cvdist.GradBuckets(self.arena.grad, [(split, self.arena.numel), (0, split)])
+            self.buckets = cvdist.GradBuckets(self.arena.grad, self.bucket_bounds())
             if self.two_nets:
                 self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)])
         # grads visible through p.grad (like the reference after loss.backward())
@@ -248,8 +249,14 @@ class ClearStep:
             self.anneal_expected = self.trainer.annealer.current_step
         return True
 
+    # batch limit of the one-workgroup label segmentation (cv_group.hip GR_MAXN); larger group batches take
+    # the module path instead of failing inside the step
+    GROUP_MAXN = 4096
+
     def accepts(self, X) -> bool:
         sp = self.spec
+        if self.mode == "group" and X.shape[0] > self.GROUP_MAXN:
+            return False
         return (X.device.type == "cuda" and X.dim() == 4 and tuple(X.shape[1:]) == (sp.in_ch, sp.H, sp.W)
                 and X.shape[0] >= 2)
 
@@ -377,10 +384,24 @@ class ClearStep:
                 prog.add("cv_tc_forward", disc, ws.z, n, ctypes.c_float(float(hp["lambda"])), ws.heads, ws.dheads,
                          d, tc_work, ws.losses.data_ptr() + 20)
         enc = Program()
-        ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer)
-        if dp:  # encoder bucket: its gradients and BN affine grads; every layer's running statistics
-            ws.step_reduce_program(enc, enc_defer, pg, "enc", running=False)
-            ws.running_program(enc, "all")
+        enc2 = None
+        if dp:
+            # the encoder gradients in two buckets at layer `k`: the heads and the deep convs (layers >= k, the
+            # bulk of the encoder's parameters) are reduced and all-reduced as soon as their weight gradients
+            # are in, while the shallow layers' backward (the big-grid GEMMs) still runs; the shallow bucket
+            # follows with every layer's running statistics
+            k = self._enc_split()
+            nl = len(sp.enc)
+            enc_defer2 = DeferGroup()
+            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, layers=range(nl - 1, k - 1, -1))
+            ws.step_reduce_program(enc, enc_defer, pg, ws.bn_enc[k:], running=False)
+            enc2 = Program()
+            ws.encoder_backward_program(enc2, pg, ws.dheads, x=X, defer=enc_defer2, heads=False,
+                                        layers=range(k - 1, -1, -1))
+            ws.step_reduce_program(enc2, enc_defer2, pg, ws.bn_enc[:k], running=False)
+            ws.running_program(enc2, "all")
+        else:
+            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer)
         upd = Program()
         if dp:
             upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
@@ -474,7 +495,7 @@ class ClearStep:
                 return gp
 
             learn, learn_inj = make_tc(False), make_tc(True)
-        return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, upd=upd, learn=learn,
+        return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, enc2=enc2, upd=upd, learn=learn,
                     fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf)
 
     def _disc_struct(self) -> cv_tc_disc:
@@ -486,6 +507,19 @@ class ClearStep:
         sp = self.spec
         return self.arena.offset[id(sp.dec_lin.weight)][0]
 
+    def _enc_split(self) -> int:
+        """First conv layer of the deep encoder bucket: the two deepest convs with the heads (VAE64: 2.9 M of
+        the encoder's 3.1 M parameters; VAE: 157 k of 176 k); layers below it form the shallow bucket."""
+        return max(len(self.spec.enc) - 2, 1)
+
+    def bucket_bounds(self):
+        """Gradient buckets in launch order (element ranges of the arena): decoder, deep encoder (the heads
+        and layers >= _enc_split()), shallow encoder."""
+        split = self._bucket_split()
+        k = self._enc_split()
+        mid = self.arena.offset[id(self.spec.enc[k].mod.weight)][0]
+        return [(split, self.arena.numel), (mid, split), (0, mid)]
+
     def _segments(self, G, inject=False):
         """The step as ('prog', [Program...]) segments and ('ar', bucket) / ('ar_est',) / ('wait',)
         points (single GPU: one segment)."""
@@ -495,8 +529,8 @@ class ClearStep:
         if self.world == 1:
             progs = [fwd, G["dec"], lat, G["enc"], G["upd"]] + ([learn] if learn is not None else [])
             return [("prog", progs)]
-        seg = [("prog", [fwd, G["dec"]]), ("ar", 0), ("prog", [lat, G["enc"]]), ("ar", 1), ("wait",),
-               ("prog", [G["upd"]])]
+        seg = [("prog", [fwd, G["dec"]]), ("ar", 0), ("prog", [lat, G["enc"]]), ("ar", 1), ("prog", [G["enc2"]]),
+               ("ar", 2), ("wait",), ("prog", [G["upd"]])]
         if learn is not None:
             for gp, ap in learn:
                 seg += [("prog", [gp]), ("ar_est",), ("wait_est",), ("prog", [ap])]
@@ -517,11 +551,25 @@ class ClearStep:
             elif kind == "ar":
                 self.buckets.launch(item[1])
             elif kind == "wait":
-                self.buckets.wait()
+                self._probe_wait(self.buckets)
             elif kind == "ar_est":
                 self.est_buckets.launch(0)
             elif kind == "wait_est":
-                self.est_buckets.wait()
+                self._probe_wait(self.est_buckets)
+
+    # comm_probe: None, or a list receiving (kind, start, end) HIP events around every wait for the gradient
+    # all-reduce on the step's stream: the exposed (not overlapped) collective time (bench.py)
+    comm_probe = None
+
+    def _probe_wait(self, buckets):
+        if self.comm_probe is None:
+            buckets.wait()
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        buckets.wait()
+        e1.record()
+        self.comm_probe.append(("vae" if buckets is self.buckets else "est", e0, e1))
 
     def _run_eager(self, G, inject=False):
         self._run_segments(self._segments(G, inject))

@@ -615,13 +615,19 @@ class Workspace:
         name = "cv_conv_backward_weight_deferred" if kind == "conv" else "cv_linear_backward_weight_deferred"
         P.add(name, geom, a, b, gw, gb, buf, buf.numel() * 4, defer.next())
 
-    def step_reduce_program(self, P: "Program", defer: "DeferGroup", param_grad, which: str = "all",
+    def _views(self, which) -> list:
+        """BN layers by name ('all', 'enc', 'dec') or an explicit list of BNViews (a gradient bucket's)."""
+        if isinstance(which, str):
+            return {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
+        return list(which)
+
+    def step_reduce_program(self, P: "Program", defer: "DeferGroup", param_grad, which="all",
                             running: bool = True, adam=None):
         """cv_step_reduce: the group's deferred weight gradients, the BN affine gradients of `which`
         layers and (running=True) their running statistics, in one launch.  adam = (params, grads, exp_avg,
         exp_avg_sq, numel, hyper, step, aux_counter): cv_step_reduce_adam, the optimizer step in the same
         launch."""
-        views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
+        views = self._views(which)
         bns = struct_array(cv_bn, [b.cv(True) for b in views])
         dg = ptr_array([param_grad(b.mod.weight) for b in views])
         db = ptr_array([param_grad(b.mod.bias) for b in views])
@@ -729,17 +735,21 @@ class Workspace:
         gout = operand(self.gah, XF_BNBWD, self.bn_1d.cv(True), y=self.h)
         P.add("cv_linear_backward_data", lin, gout, sp.dec_lin.weight, dz_out, 1, ep_none())
 
-    def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None, defer=None):
-        """From d(heads) [n, 4d] to the encoder / heads parameter gradients (and dx if asked)."""
+    def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None, defer=None, heads=True,
+                                 layers=None):
+        """From d(heads) [n, 4d] to the encoder / heads parameter gradients (and dx if asked).  A data-parallel
+        step splits it in two programs at a layer boundary (heads=False and `layers`, the conv layers in
+        backward order, for the second) so the first part's gradient bucket is reduced during the second."""
         sp, n = self.spec, self.n
         C, Hh, Wh = sp.feat
-        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
-        a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
-        self._wgrad_call(P, "linear", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
-                         param_grad(sp.heads[0].bias), ("heads",), defer)
-        ep = ep_bwd(self.bn_enc[-1], self.y_enc[-1], True, stat_div=Hh * Wh)
-        P.add("cv_linear_backward_data", lin, operand(dheads), sp.heads[0].weight, self.g_enc[-1], 0, ep)
-        for li in range(len(sp.enc) - 1, -1, -1):
+        if heads:
+            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
+            a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
+            self._wgrad_call(P, "linear", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
+                             param_grad(sp.heads[0].bias), ("heads",), defer)
+            ep = ep_bwd(self.bn_enc[-1], self.y_enc[-1], True, stat_div=Hh * Wh)
+            P.add("cv_linear_backward_data", lin, operand(dheads), sp.heads[0].weight, self.g_enc[-1], 0, ep)
+        for li in (range(len(sp.enc) - 1, -1, -1) if layers is None else layers):
             c = sp.enc[li]
             g = c.geom(n)
             gout = operand(self.g_enc[li], XF_BNBWD, self.bn_enc[li].cv(True), y=self.y_enc[li])

@@ -54,12 +54,15 @@ class DeviceImageDataset:
         return self.images.shape[0]
 
     def __getitem__(self, idx) -> tuple:
-        i = torch.tensor([int(idx)], device=self.images.device)
-        x, y, s = load_batch(self.images, i, self.size, self.labels, self.styles)
+        k, n = int(idx), len(self)
+        if not -n <= k < n:  # (list indexing semantics, like the reference's materialised list)
+            raise IndexError(f"index {k} out of range for {n} images")
+        i = torch.tensor([k % n], device=self.images.device)
+        x, y, s = load_batch(self.images, i, self.size, self.labels, self.styles, checked=False)
         return (x[0], y[0]) if s is None else (x[0], y[0], s[0])
 
-    def batch(self, index: torch.Tensor, out: torch.Tensor | None = None) -> tuple:
-        x, y, s = load_batch(self.images, index, self.size, self.labels, self.styles, out=out)
+    def batch(self, index: torch.Tensor, out: torch.Tensor | None = None, checked: bool = True) -> tuple:
+        x, y, s = load_batch(self.images, index, self.size, self.labels, self.styles, out=out, checked=checked)
         return (x, y) if s is None else (x, y, s)
 
 
@@ -87,4 +90,4 @@ class DeviceLoader:
         else:
             order = torch.arange(n, device=dev)
         for b in range(len(self)):
-            yield self.dataset.batch(order[b * self.batch_size:(b + 1) * self.batch_size])
+            yield self.dataset.batch(order[b * self.batch_size:(b + 1) * self.batch_size], checked=False)

@@ -20,7 +20,7 @@ def _np(t):
     return t.detach().double().cpu().numpy().copy()
 
 
-def run(rank, world, port, q, mode, n_global, kind):
+def run(rank, world, port, q, mode, n_global, kind, arch="VAE", precision="fp32"):
     try:
         import numpy as np
         import torch
@@ -36,14 +36,17 @@ def run(rank, world, port, q, mode, n_global, kind):
         from cvhip.engine import ClearStep
         from oracle import cpu_ref as R
         from src.models.mi_estimator import CLUBSample, L1OutUB
-        from src.models.vae import VAE
+        from cvhip.plan import set_precision
+        from src.models.vae import VAE, VAE64
         from src.trainer import ClearMIMVAETrainer, ClearTCVAETrainer, CLEARVAETrainer, HierarchicalVAETrainer
 
-        zt, C = 16, 1
-        sd = R.det_state("VAE", zt, C)
+        zt, C = (16, 1) if arch == "VAE" else (64, 3)
+        hw = R.IMAGE[arch]
+        sd = R.det_state(arch, zt, C)
         if rank != 0:  # a different start on rank 1: the engine must adopt rank 0's weights
             sd = {k: (v * 1.25 if np.asarray(v).dtype != np.int64 else v) for k, v in sd.items()}
-        vae = VAE(zt, C, group_mode=kind if mode == "group" else None).cuda()
+        vae = (VAE if arch == "VAE" else VAE64)(zt, C, group_mode=kind if mode == "group" else None).cuda()
+        set_precision(vae, precision)
         vae.load_state_dict({k: torch.as_tensor(np.asarray(v)).float() if np.asarray(v).dtype != np.int64
                              else torch.as_tensor(np.asarray(v)) for k, v in sd.items()})
         opt = torch.optim.Adam(vae.parameters(), lr=5e-4)
@@ -74,12 +77,14 @@ def run(rank, world, port, q, mode, n_global, kind):
             tr = ClearMIMVAETrainer(vae, est, {"vae_optim": opt, "mi_estimator_optim": eopt}, "cosine", hp, 1, dev)
         eng = ClearStep.build(tr, mode)
         assert eng is not None and eng.world == world, "fused DP engine not built"
+        assert eng.spec.mma == (1 if precision == "bf16" else 0)
+        assert len(eng.buckets.bounds) == 3  # decoder, deep encoder, shallow encoder
         out = {"p0": {k: _np(v) for k, v in vae.state_dict().items() if "running" not in k and "num_b" not in k}}
         if mode in ("mim", "tc"):
             out["e0"] = _np(eng.est_arena.flat)
 
         # step 1: injected noise (eager segments), this rank's contiguous shard of the global batch
-        x, label, ec, es, perm = R.det_inputs(n_global, C, 28, zt, 4, seed=21)
+        x, label, ec, es, perm = R.det_inputs(n_global, C, hw, zt, 4, seed=21)
         lo, hi = cvd.shard_bounds(n_global, rank, world)
         n = hi - lo
         rng.clear_injections()
@@ -116,10 +121,15 @@ def run(rank, world, port, q, mode, n_global, kind):
 
         # steps 2-3: device noise, graph capture + replay of the DP segments
         for s in range(2):
-            x2, l2, _, _, _ = R.det_inputs(n_global, C, 28, zt, 4, seed=30 + s)
+            x2, l2, _, _, _ = R.det_inputs(n_global, C, hw, zt, 4, seed=30 + s)
             eng.step(torch.tensor(x2[lo:hi], dtype=torch.float32, device=dev), torch.tensor(l2[lo:hi], device=dev))
         torch.cuda.synchronize()
         out["graphs"] = "graphs" in eng.graphs[n]
+        if mode in ("clear", "tc"):  # the device noise of the last step, eps = (z - mu) / exp(logvar / 2)
+            ws = eng.last_workspace(n)
+            d = zt // 2
+            h, z = ws.heads.double().cpu(), ws.z.double().cpu()
+            out["eps"] = ((z[:, :d] - h[:, :d]) / torch.exp(0.5 * h[:, d:2 * d])).numpy()
         out["p3"] = _np(eng.arena.flat)
         if mode in ("mim", "tc"):
             out["e3"] = _np(eng.est_arena.flat)

@@ -34,11 +34,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(mode, n_global, kind="CLUBSample", world=2, timeout=100):
+def _launch(mode, n_global, kind="CLUBSample", world=2, timeout=100, arch="VAE", precision="fp32"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=dp_gpu_worker.run, args=(r, world, port, q, mode, n_global, kind))
+    procs = [ctx.Process(target=dp_gpu_worker.run, args=(r, world, port, q, mode, n_global, kind, arch, precision))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -56,14 +56,14 @@ def _launch(mode, n_global, kind="CLUBSample", world=2, timeout=100):
     return res
 
 
-def _adam_ref(sd, grads, lr=5e-4):
+def _adam_ref(sd, grads, lr=5e-4, arch="VAE"):
     from oracle import cpu_ref as R
 
     P0 = R.to_torch(sd, requires_grad=False)
     names = list(grads)
     ps = [P0[k].clone().requires_grad_(True) for k in names]
     for p_, k in zip(ps, names):
-        p_.grad = torch.zeros_like(grads[k]) if _bias_before_bn(k, "VAE") else grads[k].clone()
+        p_.grad = torch.zeros_like(grads[k]) if _bias_before_bn(k, arch) else grads[k].clone()
     torch.optim.Adam(ps, lr=lr).step()
     return {k: p_.detach() for k, p_ in zip(names, ps)}
 
@@ -85,47 +85,74 @@ def _common_checks(res, sd, world=2):
     assert np.array_equal(res[0]["p3"], res[1]["p3"])
     assert res[0]["graphs"] and res[1]["graphs"], "DP segments were not graph-captured"
     assert res[0]["opt_step"] == res[1]["opt_step"] == 3
+    if "eps" in res[0]:  # each rank draws its own noise stream
+        a, b = res[0]["eps"], res[1]["eps"]
+        m = min(len(a), len(b))
+        assert not np.allclose(a[:m], b[:m], atol=1e-3)
 
 
-@pytest.mark.parametrize("n_global", [64, 50])
-def test_dp_clear_step_world2(n_global):
+DP_CLEAR = [("VAE", 64, "fp32"), ("VAE", 50, "fp32"),
+            # configs[3]'s per-rank shard (PACS: VAE64, 32 per GPU, fp32) and a bf16 VAE64 step (configs[4]'s
+            # arithmetic at a small shard)
+            ("VAE64", 64, "fp32"), ("VAE64", 32, "bf16")]
+
+
+@pytest.mark.parametrize("arch,n_global,precision", DP_CLEAR, ids=lambda v: str(v))
+def test_dp_clear_step_world2(arch, n_global, precision):
     from oracle import cpu_ref as R
+    from test_gpu_bf16 import GRAD_TOL_BF16, LOSS_TOL_BF16
 
-    res = _launch("clear", n_global)
-    sd = R.det_state("VAE", 16, 1)
+    zt, C = (16, 1) if arch == "VAE" else (64, 3)
+    res = _launch("clear", n_global, arch=arch, precision=precision, timeout=240 if arch == "VAE64" else 100)
+    sd = R.det_state(arch, zt, C)
     _common_checks(res, sd)
     hp = {"temperature": 0.1, "alpha": 100.0, "beta": 0.125, "ps": True}
-    x, label, ec, es, _ = R.det_inputs(n_global, 1, 28, 16, 4, seed=21)
+    x, label, ec, es, _ = R.det_inputs(n_global, C, R.IMAGE[arch], zt, 4, seed=21)
     shards = []
+    tol = LOSS_TOL if precision == "fp32" else LOSS_TOL_BF16
     for r in (0, 1):
         lo, hi = res[r]["bounds"]
         o = R.clear_step(R.to_torch(sd), torch.tensor(x[lo:hi]), torch.tensor(label[lo:hi]), torch.tensor(ec[lo:hi]),
-                         torch.tensor(es[lo:hi]), "VAE", hp)
+                         torch.tensor(es[lo:hi]), arch, hp)
         shards.append(o)
         got = res[r]["losses"]
         for i, k in enumerate(("rec", "kl_c", "kl_s", "c_loss", "s_loss")):
             ref = float(o[k])
-            assert abs(float(got[i]) - ref) <= LOSS_TOL * max(abs(ref), 1e-3), (r, k, float(got[i]), ref)
+            assert abs(float(got[i]) - ref) <= tol * max(abs(ref), 1e-3), (r, k, float(got[i]), ref)
     mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
-    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, "VAE")
-    ref_p = _adam_ref(sd, mean_g)
-    prel = sorted((_rel(res[0]["p1"][k], ref_p[k]), k) for k in ref_p)
-    assert prel[len(prel) // 2][0] < 1e-5, prel[-3:]
-    assert prel[-1][0] < 5e-3, prel[-3:]
+    got_g = {k: torch.tensor(v) for k, v in res[0]["grad"].items()}
+    if precision == "fp32":
+        _check_grads(got_g, mean_g, arch)
+        ref_p = _adam_ref(sd, mean_g, arch=arch)
+        prel = sorted((_rel(res[0]["p1"][k], ref_p[k]), k) for k in ref_p)
+        assert prel[len(prel) // 2][0] < 1e-5, prel[-3:]
+        assert prel[-1][0] < 5e-3, prel[-3:]
+    else:  # the bf16 bars of test_gpu_bf16.py, on the averaged gradient
+        per, num, den = [], 0.0, 0.0
+        for k, g_ref in mean_g.items():
+            if _bias_before_bn(k, arch):
+                continue
+            per.append(_rel(got_g[k], g_ref))
+            num += float((got_g[k].double() - g_ref.double()).norm() ** 2)
+            den += float(g_ref.double().norm() ** 2)
+        assert (num / den) ** 0.5 < GRAD_TOL_BF16 and sorted(per)[len(per) // 2] < GRAD_TOL_BF16, ((num / den) ** 0.5,
+                                                                                               sorted(per)[-3:])
 
 
-@pytest.mark.parametrize("kind", ["CLUBSample", "L1OutUB"])
-def test_dp_mim_step_world2(kind):
+@pytest.mark.parametrize("kind,arch", [("CLUBSample", "VAE"), ("L1OutUB", "VAE"), ("CLUBSample", "VAE64")])
+def test_dp_mim_step_world2(kind, arch):
+    """CLEAR-MIM; the VAE64 case is configs[2]'s model and estimator (CelebA 64x64, CLUB-S) at world 2."""
     from oracle import cpu_ref as R
 
-    n_global, zt = 64, 16
-    res = _launch("mim", n_global, kind)
-    sd = R.det_state("VAE", zt, 1)
+    n_global = 64 if arch == "VAE" else 32
+    zt, C = (16, 1) if arch == "VAE" else (64, 3)
+    res = _launch("mim", n_global, kind, arch=arch, timeout=240 if arch == "VAE64" else 100)
+    sd = R.det_state(arch, zt, C)
     _common_checks(res, sd)
     for key in ("e0", "e1", "e3"):
         assert np.array_equal(res[0][key], res[1][key]), key
     hp = {"temperature": 0.1, "beta": 0.125, "loc": 0, "scale": 1, "alpha": 100.0, "lambda": 3.0}
-    x, label, ec, es, _ = R.det_inputs(n_global, 1, 28, zt, 4, seed=21)
+    x, label, ec, es, _ = R.det_inputs(n_global, C, R.IMAGE[arch], zt, 4, seed=21)
     gen = np.random.default_rng(5)
     noises = [(ec, es)] + [(gen.standard_normal((n_global, zt // 2)), gen.standard_normal((n_global, zt // 2)))
                            for _ in range(5)]
@@ -134,18 +161,18 @@ def test_dp_mim_step_world2(kind):
     for r in (0, 1):
         lo, hi = res[r]["bounds"]
         o = R.mim_step(R.to_torch(sd), M0, torch.tensor(x[lo:hi]), torch.tensor(label[lo:hi]), torch.tensor(ec[lo:hi]),
-                       torch.tensor(es[lo:hi]), torch.tensor(res[r]["perm"]), "VAE", hp, kind)
+                       torch.tensor(es[lo:hi]), torch.tensor(res[r]["perm"]), arch, hp, kind)
         shards.append(o)
         got = res[r]["losses"]
         for i, k in ((0, "rec"), (1, "kl_c"), (2, "kl_s"), (3, "c_loss"), (5, "mi")):
             ref = float(o[k])
             assert abs(float(got[i]) - ref) <= LOSS_TOL * max(abs(ref), 1e-2), (r, k, float(got[i]), ref)
     mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
-    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, "VAE")
+    _check_grads({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean_g, arch)
     # the estimator: 5 x (per-shard train-mode forward with noise j on the updated VAE, per-shard
     # learning-loss gradient, mean over shards, torch Adam)
     P1 = R.to_torch(sd, requires_grad=False)
-    P1.update(_adam_ref(sd, mean_g))
+    P1.update(_adam_ref(sd, mean_g, arch=arch))
     Ps = [dict(P1), dict(P1)]
     for P in Ps:  # each rank's BN buffers evolve on its own shard
         for k in list(P):
@@ -162,7 +189,7 @@ def test_dp_mim_step_world2(kind):
             lo, hi = res[r]["bounds"]
             with torch.no_grad():
                 _, _, zz = R.vae_forward(Ps[r], torch.tensor(x[lo:hi]), torch.tensor(a[lo:hi]), torch.tensor(b[lo:hi]),
-                                         "VAE", True)
+                                         arch, True)
             ll = R.learning_loss(Md, zz[:, : zt // 2], zz[:, zt // 2:])
             g = torch.autograd.grad(ll, mparams)
             grads = [gi / 2 for gi in g] if grads is None else [acc + gi / 2 for acc, gi in zip(grads, g)]

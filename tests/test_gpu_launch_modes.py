@@ -20,7 +20,12 @@ from test_gpu_conv_kernels import TOL, _bn_state, _cvbn, _host_bnbwd, _host_bnre
 pytestmark = pytest.mark.gpu
 
 # (n, transposed, c_in, h_in, c_out, h_out, k, s, p)
-BWD = [(512, 0, 32, 14, 64, 7, 3, 2, 1), (256, 0, 32, 32, 64, 16, 4, 2, 1)]
+BWD = [(512, 0, 32, 14, 64, 7, 3, 2, 1), (256, 0, 32, 32, 64, 16, 4, 2, 1),
+       # tile counts between the one-tile and the two-tile entries' resident slots (and below both), where
+       # the two-tile grid is clamped to the tile count: MNIST conv2 at n = 256 (~784 tiles), VAE64 conv2 at
+       # n = 128 / 64
+       (256, 0, 32, 14, 64, 7, 3, 2, 1), (128, 0, 32, 32, 64, 16, 4, 2, 1), (64, 0, 32, 32, 64, 16, 4, 2, 1),
+       (384, 0, 32, 14, 64, 7, 3, 2, 1)]
 FWD = [(32, 0, 256, 4, 512, 2, 4, 2, 1), (256, 0, 256, 4, 512, 2, 4, 2, 1), (256, 1, 64, 16, 32, 32, 4, 2, 1)]
 
 
