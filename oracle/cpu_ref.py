@@ -185,22 +185,32 @@ def _bn(x, P, prefix, train):
     return out
 
 
-def encode(P, x, arch, train=True):
-    """vae.py:48-50 (encoder 15-26 / 113-130, heads 27-30)."""
+def _relu(h, masks, key):
+    """ReLU, or with masks[key] given (a 0/1 tensor of h's shape) the ReLU with its activity pattern pinned:
+    h * mask.  Pinning the pattern a device forward chose removes the knife-edge elements whose BN output
+    is within rounding of 0 from a gradient comparison (tests/test_gpu_maskpinned.py); away from such
+    elements it is the same function, so the pinned gradient is the ReLU's."""
+    if masks is not None and key in masks:
+        return h * masks[key].to(h.dtype)
+    return F.relu(h)
+
+
+def encode(P, x, arch, train=True, masks=None):
+    """vae.py:48-50 (encoder 15-26 / 113-130, heads 27-30); masks: _relu."""
     h = x
     i = 0
     for cin, cout, k, s, p in ENC[arch]:
         h = F.conv2d(h, P[f"encoder.{i}.weight"], P[f"encoder.{i}.bias"], stride=s, padding=p)
-        h = F.relu(_bn(h, P, f"encoder.{i + 1}", train))
+        h = _relu(_bn(h, P, f"encoder.{i + 1}", train), masks, f"encoder.{i + 2}")
         i += 3
     h = h.flatten(1)
     return tuple(F.linear(h, P[f"{n}.weight"], P[f"{n}.bias"]) for n in ("mu_c", "logvar_c", "mu_s", "logvar_s"))
 
 
-def decode(P, z, arch, train=True):
-    """vae.py:52-54 (decoder 32-46 / 136-156)."""
+def decode(P, z, arch, train=True, masks=None):
+    """vae.py:52-54 (decoder 32-46 / 136-156); masks: _relu."""
     h = F.linear(z, P["decoder.0.weight"], P["decoder.0.bias"])
-    h = F.relu(_bn(h, P, "decoder.1", train))
+    h = _relu(_bn(h, P, "decoder.1", train), masks, "decoder.2")
     h = h.unflatten(1, UNFLAT[arch])
     i = 4
     n_dec = len(DEC[arch])
@@ -208,7 +218,7 @@ def decode(P, z, arch, train=True):
         h = F.conv_transpose2d(h, P[f"decoder.{i}.weight"], P[f"decoder.{i}.bias"], stride=s, padding=p,
                                output_padding=op)
         h = _bn(h, P, f"decoder.{i + 1}", train)
-        h = torch.sigmoid(h) if j == n_dec - 1 else F.relu(h)
+        h = torch.sigmoid(h) if j == n_dec - 1 else _relu(h, masks, f"decoder.{i + 2}")
         i += 3
     return h
 
@@ -218,10 +228,10 @@ def sample(mu, logvar, eps):
     return mu + eps * torch.exp(0.5 * logvar)
 
 
-def vae_forward(P, x, eps_c, eps_s, arch, train=True):
-    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, train)
+def vae_forward(P, x, eps_c, eps_s, arch, train=True, masks=None):
+    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, train, masks)
     z = torch.cat([sample(mu_c, lv_c, eps_c), sample(mu_s, lv_s, eps_s)], dim=-1)
-    return decode(P, z, arch, train), {"mu_c": mu_c, "logvar_c": lv_c, "mu_s": mu_s, "logvar_s": lv_s}, z
+    return decode(P, z, arch, train, masks), {"mu_c": mu_c, "logvar_c": lv_c, "mu_s": mu_s, "logvar_s": lv_s}, z
 
 
 # ----------------------------------------------------------------------------- losses
@@ -329,9 +339,9 @@ def anneal_weight(step, beta, loc=0, scale=1):
 # ----------------------------------------------------------------------------- one training step
 
 
-def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0):
+def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0, masks=None):
     """One CLEARVAETrainer step's losses and gradients (trainer.py:452-482), no optimizer update."""
-    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True)
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks)
     rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
     c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
     s = contrastive_loss(lp["mu_s"], lp["logvar_s"], label, sim_fn, hp["temperature"], ps=hp["ps"])
@@ -347,9 +357,10 @@ def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0):
     }
 
 
-def mim_step(P, M, x, label, eps_c, eps_s, perm, arch, hp, kind="CLUBSample", sim_fn="cosine", step=0):
+def mim_step(P, M, x, label, eps_c, eps_s, perm, arch, hp, kind="CLUBSample", sim_fn="cosine", step=0,
+             masks=None):
     """The VAE half of one ClearMIMVAETrainer step (trainer.py:848-869): losses and VAE grads."""
-    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True)
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks)
     rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
     c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
     d = z.shape[1] // 2
@@ -382,10 +393,10 @@ def tc_mi_loss(D, z):
     return F.relu(torch.log(d / (1 - d))).mean()
 
 
-def tc_step(P, D, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0):
+def tc_step(P, D, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0, masks=None):
     """The VAE half of one ClearTCVAETrainer step (trainer.py:654-677): losses and VAE grads (the
     discriminator's grads of this backward are discarded by factor_optimizer.zero_grad, :682)."""
-    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True)
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks)
     rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
     c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
     mi = tc_mi_loss(D, z)
@@ -455,13 +466,13 @@ def group_order_noise(label, eps_c):
     return eps_c[order]
 
 
-def group_step(P, x, label, eps_sorted, eps_s, arch, hp, mode, step=0):
+def group_step(P, x, label, eps_sorted, eps_s, arch, hp, mode, step=0, masks=None):
     """One HierarchicalVAETrainer step's losses and gradients (trainer.py:335-353), no optimizer update:
     the ELBO on the group rows for kl_c, rec and kl_s times B/m (_group_adjust, :322-324)."""
-    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, True)
+    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, True, masks)
     mu_g, lv_g, members = group_evidence(mu_c, lv_c, label, mode)
     z = torch.cat([group_reparam(mu_g, lv_g, members, eps_sorted), sample(mu_s, lv_s, eps_s)], dim=-1)
-    xhat = decode(P, z, arch, True)
+    xhat = decode(P, z, arch, True, masks)
     rec, kl_c, kl_s = vae_loss(xhat, x, mu_g, mu_s, lv_g, lv_s)
     B, m = x.shape[0], len(members)
     rec_a, kl_s_a = rec * B / m, kl_s * B / m

@@ -123,18 +123,18 @@ def test_module_outputs_vs_golden(name):
         assert abs(float(mi) - float(fx["mi"])) <= TOL * max(abs(float(fx["mi"])), 1.0), (float(mi), float(fx["mi"]))
 
 
-@pytest.mark.parametrize("name", G.names())
-def test_fused_step_vs_golden(name):
+def build_fused(fx):
+    """The fixture's trainer and fused engine, with the case's noise (and CLUB-S permutation) queued for the
+    next step.  Returns (trainer, engine, disc or None)."""
     from cvhip import rng
     from cvhip.engine import ClearStep
     from src.trainer import ClearMIMVAETrainer, ClearTCVAETrainer, CLEARVAETrainer, HierarchicalVAETrainer
 
-    fx = G.load(name)
     m = fx["meta"]
-    arch = m["arch"]
     x, label, ec, es, perm = G.inputs(fx)
     hp = G.hyper(fx)
     vae = _model(fx)
+    disc = None
     opt = torch.optim.Adam(vae.parameters(), lr=hp["lr"])
     rng.clear_injections()
     noise = [torch.tensor(ec, dtype=torch.float32), torch.tensor(es, dtype=torch.float32)]
@@ -166,6 +166,17 @@ def test_fused_step_vs_golden(name):
         rng.inject_perm([torch.tensor(perm)])
     assert eng is not None
     rng.inject_noise(noise)
+    return tr, eng, disc
+
+
+@pytest.mark.parametrize("name", G.names())
+def test_fused_step_vs_golden(name):
+    fx = G.load(name)
+    m = fx["meta"]
+    arch = m["arch"]
+    x, label, ec, es, perm = G.inputs(fx)
+    hp = G.hyper(fx)
+    tr, eng, disc = build_fused(fx)
     X = torch.tensor(x, dtype=torch.float32, device="cuda")
     out = eng.step(X, torch.tensor(label, device="cuda"))
     losses, learn = (out, None) if m["mode"] in ("clear", "group") else out
