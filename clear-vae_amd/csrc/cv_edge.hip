@@ -17,6 +17,7 @@
 //   edge_wgrad  : part[blk][o][tap*CB + c] = sum_{px in blk} T(small[px][o]) * T(big[gather(px,tap)][c])
 //                 (both layers' weight gradients, + the conv bias column); the split partials are
 //                 summed by cv_igemm.hip's wgrad_reduce_kernel
+#include <stdlib.h>
 #include "cv_common.hpp"
 
 namespace cv {
@@ -27,6 +28,7 @@ int wgrad_reduce_launch(const float* part, int split, int M, int N, int ntot, in
 namespace edge {
 
 constexpr int ET = 256;
+__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 constexpr int CS = 32;   // small-grid channels served
 constexpr int SP = 36;   // LDS pitch (floats) of a 32-channel pixel: 16 lanes of b128 reads cover all 64 banks
 
@@ -39,7 +41,7 @@ struct EArgs {
   float* out;        // gather/scatter output; wgrad partials [blk][32][ncol]
   cv_epilogue ep;
   int rows;          // gather / wgrad: small rows per band; scatter: big rows per band
-  int ipb;           // wgrad: images per workgroup
+  int ipb;           // wgrad: images per workgroup; scatter: small rows staged per band (max)
   int ncol;          // wgrad: columns (KK*KK*CB, + 1 for the bias)
 };
 
@@ -92,7 +94,7 @@ __device__ __forceinline__ float xf_apply(int xf, float x, float y, int c, const
 template <int CB>
 __device__ __forceinline__ void stage_big(const Geo& g, const cv_operand& o, int n, int yb0, int xb0, int NR, int NC,
                                           const BnFwdC* kf, const BnBwdC* kb, float* dst) {
-  constexpr int U = 8;
+  constexpr int U = 16;  // (VAE64 gather band: 14 elements per thread in one round trip)
   const int tot = NR * NC * CB;
   const FDiv fnc = FDiv::make(NC);
   for (int base = threadIdx.x; base < tot; base += ET * U) {
@@ -123,11 +125,24 @@ __device__ __forceinline__ void stage_big(const Geo& g, const cv_operand& o, int
 }
 
 // Stage small-grid pixels [p0, p0+np) of image n (32 channels, NHWC) transformed, as dst[px*PITCH + ch].
+// Thread t always handles the channel quad 4 (t & 7) (ET is a multiple of 8), so its transform constants
+// are read from LDS once, into registers (reading them per element cost 2-way-conflicted LDS reads per
+// value); up to U float4 of x (and y) per thread are requested before the first transform.
 template <int PITCH>
 __device__ __forceinline__ void stage_small(const Geo& g, const cv_operand& o, int n, int p0, int np,
                                             const BnFwdC* kf, const BnBwdC* kb, float* dst) {
-  constexpr int U = 4;
+  constexpr int U = 8;
   const int tot4 = np * (CS / 4);
+  const int c0 = (threadIdx.x & 7) * 4;
+  BnFwdC f[4];
+  BnBwdC b[4];
+  if (o.xf == CV_XF_BNRELU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = kf[c0 + k];
+  } else if (o.xf == CV_XF_BNBWD) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b[k] = kb[c0 + k];
+  }
   const float4* x4 = reinterpret_cast<const float4*>(o.x + ((size_t)n * g.hs * g.ws + p0) * CS);
   const float4* y4 = reinterpret_cast<const float4*>(o.y ? o.y + ((size_t)n * g.hs * g.ws + p0) * CS : nullptr);
   for (int base = threadIdx.x; base < tot4; base += ET * U) {
@@ -146,12 +161,19 @@ __device__ __forceinline__ void stage_small(const Geo& g, const cv_operand& o, i
     for (int q = 0; q < U; ++q) {
       const int i = base + q * ET;
       if (i < tot4) {
-        const int px = i >> 3, c0 = (i & 7) * 4;
-        float4 r;
-        r.x = xf_apply(o.xf, v[q].x, yv[q].x, c0, kf, kb);
-        r.y = xf_apply(o.xf, v[q].y, yv[q].y, c0 + 1, kf, kb);
-        r.z = xf_apply(o.xf, v[q].z, yv[q].z, c0 + 2, kf, kb);
-        r.w = xf_apply(o.xf, v[q].w, yv[q].w, c0 + 3, kf, kb);
+        const int px = i >> 3;
+        float4 r = v[q];
+        if (o.xf == CV_XF_BNRELU) {
+          r.x = bn_relu(r.x, f[0]);
+          r.y = bn_relu(r.y, f[1]);
+          r.z = bn_relu(r.z, f[2]);
+          r.w = bn_relu(r.w, f[3]);
+        } else if (o.xf == CV_XF_BNBWD) {
+          r.x = bn_bwd(r.x, yv[q].x, b[0]);
+          r.y = bn_bwd(r.y, yv[q].y, b[1]);
+          r.z = bn_bwd(r.z, yv[q].z, b[2]);
+          r.w = bn_bwd(r.w, yv[q].w, b[3]);
+        }
         *reinterpret_cast<float4*>(dst + px * PITCH + c0) = r;
       }
     }
@@ -189,6 +211,7 @@ __device__ __forceinline__ void stats_out(const float* s1, const float* s2, doub
 // with the weights (B, <= 48 x 32) held as fragments in registers for the whole kernel and the
 // im2col operand (A) read straight out of the staged band: wave w owns pixels [64w, 64w+64) as four
 // 16-row tiles, lane l reads pixel 16i + (l&15) at tap-channel k = 4s + (l>>4).
+constexpr int GP = 36;  // LDS pitch (floats) of the gather's output tile
 template <int CB, int KK>
 __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
   constexpr int NK = KK * KK * CB;
@@ -196,7 +219,6 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
   __shared__ BnFwdC kf[4];
   __shared__ BnBwdC kb[4];
   __shared__ BnFwdC ke[CS];
-  __shared__ double scratch[4 * ET];
   __shared__ float red[ET / 64][2][CS];
   extern __shared__ __attribute__((aligned(16))) float sIn[];
   const Geo& g = P.g;
@@ -223,12 +245,14 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
     const int tap = k / CB, c = k - tap * CB, kh = tap / KK, kw = tap - kh * KK;
     koff[st] = (k < NK) ? (kh * NC + kw) * CB + c : 0;
   }
+  double* scratch = reinterpret_cast<double*>(sIn);  // (fold scratch: the staging area, unused yet)
   xf_consts(P.big, kf, kb, scratch);
   const int mode = P.ep.stat_mode;
   if (mode == CV_STAT_BWD) {
     cv_operand eo;
     eo.xf = CV_XF_BNRELU;
     eo.bn = P.ep.ebn;
+    __syncthreads();
     xf_consts(eo, ke, nullptr, scratch);
   }
   __syncthreads();
@@ -259,53 +283,83 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bw[st][j], acc[i][j], 0, 0, 0);
     }
   }
-  // epilogue: lane holds rows 4*(l>>4) + r of each 16-row tile, column 16j + (l&15)
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-  float bj[2];
+  // epilogue through LDS: the fragments (lane: rows 4*(l>>4) + r of each 16-row tile, column 16j + (l&15))
+  // are parked in a [px][GP] tile, then every thread streams 16-byte chunks of the band's output (one
+  // contiguous NHWC range) with the bias, the ReLU mask / statistics of the epilogue, and 16-byte loads of
+  // the epilogue's pre-BN tensor.  A chunk's 4 channels are c0 = 4 (t & 7) + 0..3 for every chunk a
+  // thread takes (ET is a multiple of 8), so each thread accumulates the statistics of 4 fixed channels.
+  __syncthreads();  // (every wave is done with the staged band)
+  float* sT = sIn;
+  if (64 * w < npx) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bj[j] = P.bias ? P.bias[16 * j + nl] : 0.f;
-  BnFwdC kej[2];
-  if (mode == CV_STAT_BWD) {
-    kej[0] = ke[nl];
-    kej[1] = ke[16 + nl];
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = 64 * w + 16 * i + 4 * kq + r;
+        if (px >= npx) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sT[px * GP + 16 * j + nl] = acc[i][j][r];  // (GP = 36: 4 rows -> 64 banks)
+      }
   }
+  __syncthreads();
+  const int c0 = 4 * (t & 7);
+  f32x4 b4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (P.bias) b4 = f32x4{P.bias[c0], P.bias[c0 + 1], P.bias[c0 + 2], P.bias[c0 + 3]};
+  BnFwdC kc[4];
+  if (mode == CV_STAT_BWD) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kc[k] = ke[c0 + k];
+  }
+  f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
   const size_t pimg = ((size_t)n * g.hs + r0) * g.ws;
+  const int nq = npx * (CS / 4);
+  constexpr int UQ = 4;
+  for (int q0 = t; q0 < nq; q0 += ET * UQ) {
+    f32x4 y4[UQ];
+    if (mode == CV_STAT_BWD) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int px = 64 * w + 16 * i + 4 * kq + r;
-      if (px >= npx) continue;
-      const size_t o = (pimg + px) * CS;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = 16 * j + nl;
-        float v = acc[i][j][r] + bj[j];
-        if (mode == CV_STAT_BWD) {
-          const float y = P.ep.ey[o + col];
-          if (P.ep.erelu && bn_out(y, kej[j]) <= 0.f) v = 0.f;
-          s1[j] += v;
-          s2[j] += v * ((y - kej[j].mu) * kej[j].istd);
-        } else if (mode == CV_STAT_FWD) {
-          s1[j] += v;
-          s2[j] += v * v;
-        }
-        P.out[o + col] = v;
+      for (int u = 0; u < UQ; ++u) {
+        const int q = q0 + u * ET;
+        y4[u] = q < nq ? *reinterpret_cast<const f32x4*>(P.ep.ey + (pimg + (q >> 3)) * CS + c0) : s1;
       }
     }
-  if (mode != CV_STAT_NONE) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {  // fold the four row groups (lanes l, l^16, l^32, l^48 share a column)
-      s1[j] += __shfl_xor(s1[j], 16, 64);
-      s1[j] += __shfl_xor(s1[j], 32, 64);
-      s2[j] += __shfl_xor(s2[j], 16, 64);
-      s2[j] += __shfl_xor(s2[j], 32, 64);
+    for (int u = 0; u < UQ; ++u) {
+      const int q = q0 + u * ET;
+      if (q >= nq) continue;
+      const int px = q >> 3;
+      f32x4 v = lds4(sT + px * GP + c0) + b4;
+      if (mode == CV_STAT_BWD) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (P.ep.erelu && bn_out(y4[u][k], kc[k]) <= 0.f) v[k] = 0.f;
+          s1[k] += v[k];
+          s2[k] += v[k] * ((y4[u][k] - kc[k].mu) * kc[k].istd);
+        }
+      } else if (mode == CV_STAT_FWD) {
+        s1 += v;
+        s2 += v * v;
+      }
+      *reinterpret_cast<f32x4*>(P.out + (pimg + px) * CS + c0) = v;
     }
-    if (lane < 16) {
-      red[w][0][lane] = s1[0];
-      red[w][0][16 + lane] = s1[1];
-      red[w][1][lane] = s2[0];
-      red[w][1][16 + lane] = s2[1];
+  }
+  if (mode != CV_STAT_NONE) {
+    // lanes l, l^8, l^16, ..., l^56 hold the same 4 channels: fold them, then the waves in wave order
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int m = 8; m < 64; m <<= 1) {
+        s1[k] += __shfl_xor(s1[k], m, 64);
+        s2[k] += __shfl_xor(s2[k], m, 64);
+      }
+    }
+    __syncthreads();  // (red aliases nothing, but the tile reads above must be complete before reuse below)
+    if (lane < 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        red[w][0][c0 + k] = s1[k];
+        red[w][1][c0 + k] = s2[k];
+      }
     }
     __syncthreads();
     if (t < 2 * CS) {
@@ -320,136 +374,136 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
 }
 
 // ---------------------------------------------------------------- scatter (CB outputs per pixel)
-// stride 2, even output extents, bands of an even number of big rows: wave w owns parity class
-// (w >> 1, w & 1), so its taps (and their weight words) are wave-uniform
+// ConvTranspose2d to the image (stride 2) as a gather GEMM over 2x2 output blocks.  Block (by, bx) holds
+// the four big pixels (2 by - p + cy, 2 bx - p + cx), cy, cx in {0, 1} — one of each stride-parity class
+// — and every one of them is fed by the same 2x2 small neighbourhood (by - 1 + dy, bx - 1 + dx) through
+// tap (kh, kw) = (cy + 2 - 2 dy, cx + 2 - 2 dx) (yb = 2 ys - p + kh; taps >= KK have zero weight).  So
+// the layer is one dense contraction on v_mfma_f32_16x16x4_f32: M = blocks, K = 4 neighbours x 32
+// channels, N = 4 classes x CB output channels (12 of 16 columns for CB = 3), the weights held as B
+// fragments in registers for the whole kernel and the A fragments read from the band's small rows
+// staged in LDS (BN + ReLU applied once there).  Blocks partition the big pixels, so every output is
+// written once, with its bias, into an LDS tile of the band's big rows, which leave in 16-byte stores
+// (one contiguous NHWC range) together with the statistics epilogue.
+// (Round 2 ran this layer as per-class VALU dot products — 4x the FMAs' own instruction count issued,
+// ~54 us on the VAE64 layer; a col2im variant through LDS read-modify-writes measured 70 us.)
 template <int CB, int KK>
 __global__ __launch_bounds__(ET) void edge_scatter_kernel(const EArgs P) {
-  constexpr int NK = KK * KK;
-  __shared__ float4 sW[NK * CB * 8];  // [tap][cb][32]
-  __shared__ float sbias[4];
+  constexpr int NCOL = 4 * CB;  // GEMM columns: class (2 cy + cx) * CB + output channel
+  static_assert(NCOL <= 16 && KK <= 4, "one 16-column tile; taps cy + 2 - 2 dy < 4");
   __shared__ BnFwdC kf[CS];
   __shared__ BnBwdC kb[CS];
-  __shared__ BnFwdC ke[4];
-  __shared__ double scratch[4 * ET];
+  __shared__ float sb[4];
   __shared__ float red[(ET / 64) * 2 * 4];
   extern __shared__ __attribute__((aligned(16))) float sIn[];
   const Geo& g = P.g;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kq = lane >> 4, nl = lane & 15;
   const int n = blockIdx.y;
-  const int B0 = blockIdx.x * P.rows;
-  const int RB = min(P.rows, g.hb - B0);
-  // small rows feeding big rows [B0, B0+RB)
-  const int num = B0 + g.p - (KK - 1);
-  const int ys_lo = num <= 0 ? 0 : (num + 1) / 2;
-  const int ys_hi = min(g.hs - 1, (B0 + RB - 1 + g.p) / 2);
+  const int nby = (g.hb - 1 + g.p) / 2 + 1, nbx = (g.wb - 1 + g.p) / 2 + 1;  // block rows / columns
+  const int bb0 = blockIdx.x * P.rows;
+  const int RBb = min(P.rows, nby - bb0);
+  // small rows [ys_lo, ys_hi] feed block rows [bb0, bb0 + RBb); big rows [yb0, yb1) are the band's output
+  const int ys_lo = max(bb0 - 1, 0), ys_hi = min(bb0 + RBb - 1, g.hs - 1);
   const int nrs = ys_hi - ys_lo + 1;
-  // weights: packed scatter layout [tap][cs][cb] -> [tap][cb][cs]
-  for (int i = t; i < NK * CB * CS; i += ET) {
-    const int tap = i / (CB * CS), r = i - tap * CB * CS, cb = r / CS, cs = r - cb * CS;
-    reinterpret_cast<float*>(sW)[i] = P.w[(tap * CS + cs) * CB + cb];
+  const int yb0 = max(2 * bb0 - g.p, 0), yb1 = min(2 * (bb0 + RBb) - g.p, g.hb);
+  float* sOut = sIn + (size_t)P.ipb * g.ws * SP;  // [yb1 - yb0][wb][CB]
+  // B fragments: neighbour q = 2 dy + dx, k-step s: lane (kq, nl) holds W[tap(q, class nl / CB)][ch 8 kq + s][nl % CB].
+  // The block matrix W'[col][q * 32 + ch] is built once per workgroup in LDS from the packed scatter layout
+  // [tap][cs][cb] (coalesced reads of the KK*KK*32*CB weights), pitch WKP: the 16 lanes of a b128 read hit
+  // 16 disjoint 4-bank groups
+  constexpr int WKP = 4 * CS + 4;
+  float* sWb = sIn + 4 * ET * 2;  // [16][WKP] behind the fold scratch, inside the (not yet used) staging area
+  for (int i = t; i < 16 * 4 * CS; i += ET) {
+    const int col = i / (4 * CS), k = i - col * (4 * CS), q = k / CS, ch = k - q * CS;
+    const int c2 = col / CB, c3 = col - c2 * CB;
+    const int kh = (c2 >> 1) + 2 - 2 * (q >> 1), kw = (c2 & 1) + 2 - 2 * (q & 1);
+    sWb[col * WKP + k] = (col < NCOL && kh < KK && kw < KK) ? P.w[((kh * KK + kw) * CS + ch) * CB + c3] : 0.f;
   }
-  if (t < CB) sbias[t] = P.bias ? P.bias[t] : 0.f;
-  xf_consts(P.small, kf, kb, scratch);
-  const int mode = P.ep.stat_mode;
-  if (mode == CV_STAT_BWD) {
-    cv_operand eo;
-    eo.xf = CV_XF_BNRELU;
-    eo.bn = P.ep.ebn;
-    xf_consts(eo, ke, nullptr, scratch);
-  }
+  const int cls = nl / CB, cb = nl - cls * CB, cy = cls >> 1, cx = cls & 1;
+  if (t < CB) sb[t] = P.bias ? P.bias[t] : 0.f;
+  xf_consts(P.small, kf, kb, reinterpret_cast<double*>(sIn));  // (fold scratch: the staging area, unused yet)
   __syncthreads();
-  float* sOut = sIn + (size_t)(P.rows / 2 + (KK + 1) / 2 + 1) * g.ws * SP;  // [RB][wb][CB]
+  float bw[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 w0 = lds4(sWb + nl * WKP + q * CS + 8 * kq), w1 = lds4(sWb + nl * WKP + q * CS + 8 * kq + 4);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      bw[q][st] = w0[st];
+      bw[q][st + 4] = w1[st];
+    }
+  }
+  __syncthreads();  // (the staging below overwrites the block matrix)
   if (nrs > 0) stage_small<SP>(g, P.small, n, ys_lo * g.ws, nrs * g.ws, kf, kb, sIn);
   __syncthreads();
+  const float bias = nl < NCOL ? sb[cb] : 0.f;
+  const int nblk = RBb * nbx, ntile = (nblk + 15) / 16;
+  const FDiv fnbx = FDiv::make(nbx);
+  for (int tile = w; tile < ntile; tile += 4) {
+    // A: this lane's block (row nl of the tile), channels 8 kq .. 8 kq + 7 of each neighbour
+    const int blk = 16 * tile + nl;
+    const int br = fnbx.div(blk), bx = blk - br * nbx, by = bb0 + br;
+    // one accumulator per neighbour: four independent MFMA chains (a single chain of 32 dependent MFMAs
+    // leaves the matrix pipe waiting on its own results), summed in neighbour order
+    f32x4 accq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      accq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int ys = by - 1 + (q >> 1), xs = bx - 1 + (q & 1);
+      const bool ok = blk < nblk && ys >= ys_lo && ys <= ys_hi && (unsigned)xs < (unsigned)g.ws;
+      const float* ap = sIn + (ok ? ((ys - ys_lo) * g.ws + xs) * SP + 8 * kq : 0);  // (SP = 36: conflict-free)
+      f32x4 a0 = lds4(ap), a1 = lds4(ap + 4);
+      if (!ok) a0 = a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 8; ++st)
+        accq[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(st < 4 ? a0[st] : a1[st - 4], bw[q][st], accq[q], 0, 0, 0);
+    }
+    const f32x4 acc = (accq[0] + accq[1]) + (accq[2] + accq[3]);
+    // acc[r]: block 16 tile + 4 kq + r, column nl = (class, cb)
+    if (nl < NCOL) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b2 = 16 * tile + 4 * kq + r;
+        if (b2 >= nblk) continue;
+        const int r2 = fnbx.div(b2), x2 = b2 - r2 * nbx;
+        const int yb = 2 * (bb0 + r2) - g.p + cy, xb = 2 * x2 - g.p + cx;
+        if (yb >= yb0 && yb < yb1 && (unsigned)xb < (unsigned)g.wb)
+          sOut[((yb - yb0) * g.wb + xb) * CB + cb] = acc[r] + bias;
+      }
+    }
+  }
+  __syncthreads();
+  // the band's output rows are one contiguous range: 16-byte stores (+ the statistics epilogue)
+  const int mode = P.ep.stat_mode;
   float s1[CB], s2[CB];
 #pragma unroll
   for (int j = 0; j < CB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  const int ry = w >> 1, rx = w & 1;
-  const int ky0 = (ry + g.p) & 1, kx0 = (rx + g.p) & 1;  // B0 even: the class's first tap row / column
-  const int cy = (RB - ry + 1) / 2, cx = (g.wb - rx + 1) / 2;
-  const int ncls = cy * cx;
-  constexpr int TH = (KK + 1) / 2;  // taps per class and direction
-  constexpr int PPL = 4;            // class pixels per lane: each weight word read feeds 4 pixels
-  for (int q0 = 0; q0 < ncls; q0 += 64 * PPL) {
-    int yb[PPL], xb[PPL];
-    bool live[PPL];
-    float acc[PPL][CB];
+  const int tot = (yb1 - yb0) * g.wb * CB;
+  float* dst = P.out + (size_t)(n * g.hb + yb0) * g.wb * CB;
+  const int tot4 = tot >> 2;
+  for (int i = t; i < tot4; i += ET) {
+    const f32x4 v = lds4(sOut + 4 * i);
+    *reinterpret_cast<f32x4*>(dst + 4 * i) = v;
+    if (mode == CV_STAT_FWD) {
 #pragma unroll
-    for (int u = 0; u < PPL; ++u) {
-      const int q = q0 + 64 * u + lane;
-      live[u] = q < ncls;
-      const int iy = q / cx, ix = q - iy * cx;
-      yb[u] = B0 + ry + 2 * iy;
-      xb[u] = rx + 2 * ix;
+      for (int k = 0; k < 4; ++k) {
+        const int j = (4 * i + k) % CB;
 #pragma unroll
-      for (int j = 0; j < CB; ++j) acc[u][j] = sbias[j];
-    }
-#pragma unroll 1
-    for (int jy = 0; jy < TH; ++jy) {
-      const int kh = ky0 + 2 * jy;
-      if (kh >= KK) continue;
-#pragma unroll 1
-      for (int jx = 0; jx < TH; ++jx) {
-        const int kw = kx0 + 2 * jx;
-        if (kw >= KK) continue;
-        const float4* src[PPL];
-        bool ok[PPL];
-#pragma unroll
-        for (int u = 0; u < PPL; ++u) {
-          const int ys = (yb[u] + g.p - kh) >> 1, xs = (xb[u] + g.p - kw) >> 1;
-          ok[u] = live[u] && ys >= 0 && ys < g.hs && xs >= 0 && xs < g.ws;
-          src[u] = reinterpret_cast<const float4*>(sIn + (ok[u] ? ((ys - ys_lo) * g.ws + xs) * SP : 0));
-        }
-        const float4* wr = sW + (kh * KK + kw) * CB * 8;
-#pragma unroll 2
-        for (int c4 = 0; c4 < 8; ++c4) {
-          float4 x4[PPL];
-#pragma unroll
-          for (int u = 0; u < PPL; ++u) x4[u] = ok[u] ? src[u][c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-          for (int j = 0; j < CB; ++j) {
-            const float4 w4 = wr[j * 8 + c4];
-#pragma unroll
-            for (int u = 0; u < PPL; ++u) {
-              acc[u][j] = fmaf(x4[u].x, w4.x, acc[u][j]);
-              acc[u][j] = fmaf(x4[u].y, w4.y, acc[u][j]);
-              acc[u][j] = fmaf(x4[u].z, w4.z, acc[u][j]);
-              acc[u][j] = fmaf(x4[u].w, w4.w, acc[u][j]);
-            }
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < PPL; ++u) {
-      if (!live[u]) continue;
-      const size_t po = ((size_t)(n * g.hb + yb[u]) * g.wb + xb[u]) * CB;
-      const int lo = ((yb[u] - B0) * g.wb + xb[u]) * CB;
-#pragma unroll
-      for (int j = 0; j < CB; ++j) {
-        float v = acc[u][j];
-        if (mode == CV_STAT_BWD) {
-          const float yv = P.ep.ey[po + j];
-          if (P.ep.erelu && bn_out(yv, ke[j]) <= 0.f) v = 0.f;
-          s1[j] += v;
-          s2[j] += v * ((yv - ke[j].mu) * ke[j].istd);
-        } else if (mode == CV_STAT_FWD) {
-          s1[j] += v;
-          s2[j] += v * v;
-        }
-        sOut[lo + j] = v;
+        for (int c = 0; c < CB; ++c)
+          if (c == j) { s1[c] += v[k]; s2[c] += v[k] * v[k]; }
       }
     }
   }
-  // the band's output rows are one contiguous range: stored after every weight load (no global
-  // store before them lets the compiler keep the wave-uniform weights on the scalar path)
-  __syncthreads();
-  {
-    const int tot = RB * g.wb * CB;
-    float* dst = P.out + (size_t)(n * g.hb + B0) * g.wb * CB;
-    for (int i = t; i < tot; i += ET) dst[i] = sOut[i];
+  for (int i = 4 * tot4 + t; i < tot; i += ET) {
+    const float v = sOut[i];
+    dst[i] = v;
+    if (mode == CV_STAT_FWD) {
+      const int j = i % CB;
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+        if (c == j) { s1[c] += v; s2[c] += v * v; }
+    }
   }
-  if (mode != CV_STAT_NONE) stats_out<CB>(s1, s2, P.ep.stat_out, CB, red);
+  if (mode == CV_STAT_FWD) stats_out<CB>(s1, s2, P.ep.stat_out, CB, red);
 }
 
 // ---------------------------------------------------------------- weight gradient (split partials)
@@ -616,7 +670,10 @@ int edge_gather(const Geo& g, const cv_operand* in, const float* wg, const float
   a.rows = g.ws >= ET ? 1 : ET / g.ws;
   if (a.rows > g.hs) a.rows = g.hs;
   const int kk = g.kh, cb = g.cb;
-  const size_t lds = (size_t)((a.rows - 1) * g.s + kk) * ((g.ws - 1) * g.s + kk) * cb * sizeof(float);
+  size_t lds = (size_t)((a.rows - 1) * g.s + kk) * ((g.ws - 1) * g.s + kk) * cb * sizeof(float);
+  const size_t tile = (size_t)a.rows * g.ws * GP * sizeof(float);  // the epilogue's output tile
+  if (tile > lds) lds = tile;
+  if (lds < 4 * ET * sizeof(double)) lds = 4 * ET * sizeof(double);  // (BN fold scratch)
   if (lds > 96 * 1024) return -1;
   const void* kern = nullptr;
   CV_EDGE_PICK(edge_gather_kernel);
@@ -625,7 +682,9 @@ int edge_gather(const Geo& g, const cv_operand* in, const float* wg, const float
 
 int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
                  const cv_epilogue* ep, hipStream_t st) {
+  // (the statistics epilogue of this layer is the forward one: the decoder's output BatchNorm)
   if (!geo_ok(g) || g.s != 2 || (g.hb & 1) || (g.wb & 1) || !ep_ok(ep, g.cb)) return -1;
+  if (ep && ep->stat_mode == CV_STAT_BWD) return -1;
   if (in->nchw || (in->xf != CV_XF_NONE && in->bn.C != CS) || (in->xf == CV_XF_BNBWD && !in->y)) return -1;
   EArgs a;
   memset(&a, 0, sizeof(a));
@@ -636,19 +695,38 @@ int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const floa
   a.out = out;
   if (ep) a.ep = *ep;
   else a.ep.stat_mode = CV_STAT_NONE;
-  // bands of an even number of big rows, ~1024 output pixels each
-  int rb = (4 * ET) / g.wb;
-  rb &= ~1;
-  if (rb < 2) rb = 2;
-  if (rb > g.hb) rb = g.hb;
-  a.rows = rb;
   const int kk = g.kh, cb = g.cb;
-  const int nrs = rb / 2 + (kk + 1) / 2 + 1;
-  const size_t lds = ((size_t)nrs * g.ws * SP + (size_t)rb * g.wb * cb) * sizeof(float);
+  // bands of block rows (2 big rows each): as many as fit ~36 KB of staged small rows (VAE64: 7 block rows
+  // = 8 small rows, 3-4 workgroups per CU; MNIST: a whole image), shortened while the grid has fewer than
+  // 512 workgroups (down to 2).  CV_EDGE_SCATTER_RB=<rows> overrides (A/B knob).
+  const int nby = (g.hb - 1 + g.p) / 2 + 1;
+  if (kk > 4 || 4 * cb > 16 || g.p < 0 || g.p > 2) return -1;
+  int rb = (36 * 1024) / (g.ws * SP * (int)sizeof(float)) - 1;
+  if (rb > nby) rb = nby;
+  if (rb < 1) rb = 1;
+  while (rb > 2 && (long)g.n * cdiv(nby, rb) < 512) {
+    const int r2 = (rb + 1) / 2;
+    if (r2 >= rb) break;
+    rb = r2;
+  }
+  rb = cdiv(nby, cdiv(nby, rb));  // even bands
+  {
+    static int ovr = -2;
+    if (ovr == -2) {
+      const char* e = getenv("CV_EDGE_SCATTER_RB");
+      ovr = e ? atoi(e) : -1;
+    }
+    if (ovr > 0) rb = ovr < nby ? ovr : nby;
+  }
+  a.rows = rb;
+  a.ipb = rb + 1;  // (scatter: small rows staged per band, sizes the LDS carve-up)
+  size_t lds = ((size_t)a.ipb * g.ws * SP + (size_t)2 * rb * g.wb * cb) * sizeof(float);
+  const size_t pre = 4 * ET * sizeof(double) + 16 * (4 * CS + 4) * sizeof(float);  // fold scratch + block matrix
+  if (lds < pre) lds = pre;
   if (lds > 96 * 1024) return -1;
   const void* kern = nullptr;
   CV_EDGE_PICK(edge_scatter_kernel);
-  return launch(kern, dim3(cdiv(g.hb, rb), g.n), lds, a, st, "edge_scatter");
+  return launch(kern, dim3(cdiv(nby, rb), g.n), lds, a, st, "edge_scatter");
 }
 
 static int edge_rows(const Geo& g) {
