@@ -428,7 +428,8 @@ int launch_fast(const Args& a, dim3 grid, hipStream_t st) {
   }
   if constexpr (OP == OP_GATHER || OP == OP_SCATTER) {
     const long tiles = (long)grid.x * grid.y * grid.z;
-    if (persist_enabled() && tiles > resident_slots((const void*)kern, lds)) {
+    // (a K-split launch keeps one tile per workgroup: its slices meet through the tile's ticket)
+    if (persist_enabled() && !a.fix_part && tiles > resident_slots((const void*)kern, lds)) {
       auto kern2 = gemm_kernel2<OP, BM, BN, XA, XB, EPI, DEPTH, MT>;
       const long slots = resident_slots((const void*)kern2, lds);
       if (slots > 0) {

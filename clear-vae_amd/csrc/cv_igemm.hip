@@ -994,6 +994,50 @@ static int check_conv(const cv_conv* g) {
   return 0;
 }
 
+// Per-device workspace of the in-launch split-K (cv_set_gemm_workspace): fragment slabs + per-tile tickets.
+// Borrowed from the caller (the library never allocates); GATHER launches on one stream use it one at a time.
+constexpr int FIX_MAX_DEV = 16;
+constexpr size_t FIX_CNT_WORDS = 4096;  // tickets (zeroed by the caller at registration; self-resetting)
+static void* g_fix_work[FIX_MAX_DEV];
+static size_t g_fix_bytes[FIX_MAX_DEV];
+
+static bool fix_workspace(float*& part, unsigned*& cnt, size_t& part_bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= FIX_MAX_DEV) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (!g_fix_work[dev] || g_fix_bytes[dev] <= FIX_CNT_WORDS * 4) return false;
+  cnt = static_cast<unsigned*>(g_fix_work[dev]);
+  part = reinterpret_cast<float*>(static_cast<char*>(g_fix_work[dev]) + FIX_CNT_WORDS * 4);
+  part_bytes = g_fix_bytes[dev] - FIX_CNT_WORDS * 4;
+  return true;
+}
+
+// K slices of an under-filled long-K GATHER: the launch's tiles use less than half of the chip's CUs and
+// each would walk >= 16 K tiles alone (VAE64's deep layers at small batches: conv5 forward at 32-256
+// images/GPU is 16-128 tiles of K = 4096).  Powers of two while tiles x slices <= 2 x CUs and every slice
+// keeps >= 8 K tiles.  CV_SPLITK=0: off (A/B).
+static int gather_split(long tiles, int ktiles) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("CV_SPLITK");
+    mode = e ? atoi(e) : 1;
+  }
+  if (mode == 0 || g_force_generic || ktiles < 16) return 1;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    (void)hipGetLastError();
+  }
+  if (2 * tiles > cus) return 1;
+  int s = 1;
+  while (tiles * s * 2 <= 2L * cus && ktiles / (s * 2) >= 8 && s < 16) s *= 2;
+  return s;
+}
+
 // GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
 static int run_gather(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                       const cv_epilogue* ep, hipStream_t st, const char* what, int mma) {
@@ -1021,6 +1065,32 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
   int BM_, BN_;
   pick_tile(a.M, a.N, BM_, BN_);
   a.kchunk = ((a.K + BK - 1) / BK) * BK;
+  // long K (>= 32 K tiles): wide 64-column tiles split along K fill the chip with 4x fewer passes over the
+  // A operand than the narrow tiles pick_tile shrinks to for parallelism (C5's conv5 forward: 64 tiles x 4
+  // slices of 32 K tiles instead of 256 tiles of 128)
+  if (a.K % BK == 0 && a.K / BK >= 32 && a.N >= 64 && BN_ < 64) {
+    const long t64 = (long)cdiv(a.M, 64) * cdiv(a.N, 64);
+    if (t64 * gather_split(t64, a.K / BK) >= (long)cdiv(a.M, BM_) * cdiv(a.N, BN_)) {
+      BM_ = 64;
+      BN_ = 64;
+    }
+  }
+  const long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
+  const int split = (a.K % BK == 0) ? gather_split(tiles, a.K / BK) : 1;
+  float* part = nullptr;
+  unsigned* cnt = nullptr;
+  size_t pbytes = 0;
+  if (split > 1 && tiles <= (long)FIX_CNT_WORDS && fix_workspace(part, cnt, pbytes) &&
+      (size_t)tiles * split * BM_ * BN_ * sizeof(float) <= pbytes) {
+    Args s = a;
+    s.kchunk = cdiv(a.K / BK, split) * BK;
+    s.fix_part = part;
+    s.fix_cnt = cnt;
+    finalize_divs(s);
+    const dim3 grid(cdiv(s.M, BM_), cdiv(s.N, BN_), cdiv(a.K, s.kchunk));
+    const int r = gemm_fast_gather(s, BM_, BN_, grid, st);  // (the generic kernel has no slab combine)
+    if (r >= 0) return r;
+  }
   return launch(a, BM_, BN_, 1, st);
 }
 
@@ -1050,6 +1120,34 @@ static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const
   if (apply_epilogue(a, ep, a.N, what)) return 1;
   int BM_, BN_;
   pick_tile((long)a.M * g.s * g.s, a.N, BM_, BN_);
+  // in-launch split-K as in run_gather, for kernels whose stride-parity classes all have the same taps
+  // (kh, kw multiples of the stride: every class has K = a.K) and even class extents
+  const int ss = g.s * g.s;
+  if (g.kh % g.s == 0 && g.kw % g.s == 0 && g.hb % g.s == 0 && g.wb % g.s == 0 && a.K % BK == 0 && a.K / BK >= 32) {
+    if (a.N >= 64 && BN_ < 64) {
+      const long t64 = (long)cdiv(a.M, 64) * cdiv(a.N, 64) * ss;
+      if (t64 * gather_split(t64, a.K / BK) >= (long)cdiv(a.M, BM_) * cdiv(a.N, BN_) * ss) {
+        BM_ = 64;
+        BN_ = 64;
+      }
+    }
+    const long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_) * ss;
+    const int split = gather_split(tiles, a.K / BK);
+    float* part = nullptr;
+    unsigned* cnt = nullptr;
+    size_t pbytes = 0;
+    if (split > 1 && tiles <= (long)FIX_CNT_WORDS && fix_workspace(part, cnt, pbytes) &&
+        (size_t)tiles * split * BM_ * BN_ * sizeof(float) <= pbytes) {
+      Args s = a;
+      s.kchunk = cdiv(a.K / BK, split) * BK;
+      s.fix_part = part;
+      s.fix_cnt = cnt;
+      finalize_divs(s);
+      const dim3 grid(cdiv(s.M, BM_), cdiv(s.N, BN_), ss * cdiv(a.K, s.kchunk));
+      const int r = gemm_fast_scatter(s, BM_, BN_, grid, st);
+      if (r >= 0) return r;
+    }
+  }
   return launch(a, BM_, BN_, g.s * g.s, st);
 }
 
@@ -1190,6 +1288,22 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
 }  // namespace cv
 
 using namespace cv;
+
+extern "C" size_t cv_gemm_workspace_bytes(void) {
+  // 512 slices of one 64 x 64 fp32 tile each + the ticket words
+  return FIX_CNT_WORDS * 4 + (size_t)512 * 64 * 64 * sizeof(float);
+}
+
+extern "C" int cv_set_gemm_workspace(void* work, size_t bytes) {
+  clear_error();
+  int dev = 0;
+  CV_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < FIX_MAX_DEV, "set_gemm_workspace: no device");
+  CV_REQUIRE(!work || bytes > FIX_CNT_WORDS * 4, "set_gemm_workspace: %zu bytes is too small", bytes);
+  CV_REQUIRE(!work || (reinterpret_cast<uintptr_t>(work) & 15) == 0, "set_gemm_workspace: pointer not 16-byte aligned");
+  g_fix_work[dev] = work;
+  g_fix_bytes[dev] = work ? bytes : 0;
+  return 0;
+}
 
 extern "C" int cv_debug_force_generic_gemm(int on) {
   const int prev = g_force_generic;

@@ -48,6 +48,11 @@ struct Args {
   int ca_n, cb_n, ce_n;      // feature counts of a / b / epilogue BN constants (0 = unused)
   int mma;                   // CV_MMA_FP32 / CV_MMA_BF16 operand precision of the specialised core
   int tiles_x, tiles_y, tiles_z;  // two-tile launch of the specialised core (gemm_kernel2): the tile grid
+  // in-launch split-K of an under-filled long-K GATHER (specialised one-tile core only): gridDim.z slices of
+  // kchunk; each slice leaves its fragment slab in fix_part, the last of a tile's slices (fix_cnt ticket)
+  // sums the slabs in slice order and runs the epilogue.  Null: no split.
+  float* fix_part;
+  unsigned* fix_cnt;
   // fast divisors (filled by finalize_divs at launch)
   FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
 };

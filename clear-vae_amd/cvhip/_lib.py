@@ -297,6 +297,8 @@ _SIGS = {
     "cv_last_error": (ctypes.c_char_p, []),
     "cv_version": (c_int, []),
     "cv_debug_force_generic_gemm": (c_int, [c_int]),
+    "cv_gemm_workspace_bytes": (c_size_t, []),
+    "cv_set_gemm_workspace": (c_int, [c_void_p, c_size_t]),
 }
 
 EXPORTED = tuple(_SIGS)
@@ -347,6 +349,23 @@ def ptr(t) -> int | None:
     if t is None:
         return None
     return t.data_ptr()
+
+
+_GEMM_WS: dict = {}
+
+
+def ensure_gemm_workspace(device) -> None:
+    """Register the device's GEMM workspace with the library once (cv_set_gemm_workspace: the in-launch
+    split-K of under-filled long-K convolutions); a zeroed torch buffer kept alive for the process."""
+    device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _GEMM_WS:
+        return
+    nbytes = int(lib().cv_gemm_workspace_bytes())
+    buf = torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=torch.device("cuda", idx))
+    with torch.cuda.device(idx):
+        call("cv_set_gemm_workspace", buf.data_ptr(), buf.numel() * 4)
+    _GEMM_WS[idx] = buf
 
 
 def stream_handle() -> int:

@@ -522,6 +522,7 @@ class Workspace:
 
     def __init__(self, spec: VaeSpec, n: int, device, with_grad: bool = True):
         self.spec, self.n, self.device = spec, n, device
+        _lib.ensure_gemm_workspace(device)
         f32 = dict(dtype=torch.float32, device=device)
         d = spec.d
         self.y_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]

@@ -458,6 +458,14 @@ int cv_version(void);
  * specialised core (both compute the same contraction); returns the previous setting */
 int cv_debug_force_generic_gemm(int on);
 
+/* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
+ * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least
+ * cv_gemm_workspace_bytes(), ZEROED before registration, for the current device (NULL: unregister).
+ * Calls on one stream share it; without one the launches run unsplit.  No reference counterpart
+ * (the reference's convolutions are ATen's, code/src/models/vae.py:15-46 / :113-156). */
+size_t cv_gemm_workspace_bytes(void);
+int cv_set_gemm_workspace(void* work, size_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,3 +26,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _gemm_workspace(request):
+    """GPU tests run with the library's GEMM workspace registered, as the engine runs (the in-launch
+    split-K of long-K convolutions is then exercised by the kernel tests too)."""
+    if "gpu" in request.keywords:
+        import torch
+
+        if torch.cuda.is_available():
+            from cvhip import _lib
+
+            _lib.ensure_gemm_workspace(torch.device("cuda", 0))
+    yield
