@@ -112,9 +112,19 @@ def contrastive_loss(mu: torch.Tensor, logvar: torch.Tensor, label: torch.Tensor
     masks, masked log-sum-exps and the mean over finite rows, with its analytic backward."""
     if sim_fn not in SIM:
         raise ValueError("unimplemented similarity measure.")
+    if loss_name in ("supcon_in_loss", "supcon_out_loss"):
+        # Off the trained path (no trainer or script passes them: SURVEY 2b): the reference's own composition
+        # (losses.py:107-126 with its eval(loss_name) dispatch) over the pairwise / supcon functions below, as
+        # torch ops on the caller's tensors, so a caller naming them gets the reference's values.
+        pair_mat = (label[None, :] != label[:, None]).float() if ps else (label[None, :] == label[:, None]).float()
+        sim = {"cosine": lambda: pairwise_cosine(mu), "l2": lambda: pairwise_l2(mu),
+               "modified_l2": lambda: pairwise_modified_l2_dis(mu, logvar),
+               "jeffrey": lambda: pairwise_jeffrey_div(mu, logvar),
+               "mahalanobis": lambda: pairwise_mahalanobis_dis(mu, logvar)}[sim_fn]()
+        losses = (supcon_in_loss if loss_name == "supcon_in_loss" else supcon_out_loss)(sim, pair_mat, temperature)
+        return losses[torch.isfinite(losses)].mean()
     if loss_name != "snn_loss":
-        # the reference's only trained loss; supcon variants are defined but never called (SURVEY 2b)
-        raise NotImplementedError(f"{loss_name} is not on the HIP path (only snn_loss)")
+        raise NameError(f"name '{loss_name}' is not defined")  # (what the reference's eval(loss_name) raises)
     _ag._require_gpu(mu, logvar, label)
     return _ag.ContrastiveFn.apply(mu, logvar, label, sim_fn, temperature, bool(ps))
 
