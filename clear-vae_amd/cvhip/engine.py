@@ -508,9 +508,19 @@ class ClearStep:
         return self.arena.offset[id(sp.dec_lin.weight)][0]
 
     def _enc_split(self) -> int:
-        """First conv layer of the deep encoder bucket: the two deepest convs with the heads (VAE64: 2.9 M of
-        the encoder's 3.1 M parameters; VAE: 157 k of 176 k); layers below it form the shallow bucket."""
-        return max(len(self.spec.enc) - 2, 1)
+        """First conv layer of the deep encoder bucket: the deepest layers that, with the heads, hold >= 80 % of
+        the encoder's parameters (VAE64: conv4, conv5 + heads, 2.9 M of 3.1 M; VAE: conv3 + heads, 140 k of
+        158 k).  The deep bucket's all-reduce runs while the shallow layers' backward (the big-grid GEMMs)
+        still runs; the shallow bucket (VAE64 0.66 MB, VAE 75 KB) is the exposed part."""
+        sp = self.spec
+        size = [c.mod.weight.numel() + c.mod.bias.numel() + 2 * c.bn.num_features for c in sp.enc]
+        heads = sum(h.weight.numel() + h.bias.numel() for h in sp.heads)
+        total = sum(size) + heads
+        k, acc = len(sp.enc), heads
+        while k > 1 and acc < 0.8 * total:
+            k -= 1
+            acc += size[k]
+        return k if k < len(sp.enc) else len(sp.enc) - 1
 
     def bucket_bounds(self):
         """Gradient buckets in launch order (element ranges of the arena): decoder, deep encoder (the heads
