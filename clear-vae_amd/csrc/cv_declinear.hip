@@ -1,0 +1,655 @@
+// The latent-side linear blocks of the fused step, each in one launch:
+//   decoder input forward : z = mu + eps * exp(logvar / 2)               (VAE.sample, code/src/models/vae.py:56-60)
+//                           h = Linear(z) -> BatchNorm1d -> ReLU -> ah   (vae.py:33-35; Unflatten :36 = storage order)
+//   decoder input backward: ReLU mask, BatchNorm1d backward sums and transform, Linear weight gradient
+//                           (dz = d(h) W stays a DENSE GEMM: it reduces over every feature)
+//   encoder heads backward: d(flat) = dheads W with the last block's ReLU mask and BN backward sums, the heads'
+//                           weight and bias gradients (vae.py:25-30)
+//
+// A workgroup owns DF = 16 storage columns of the [n][F] activation for ALL n rows.  The BatchNorm1d
+// statistics of its features are therefore complete inside the workgroup: the decoder-input forward applies the
+// normalisation in the same launch (it was Linear + a separate cv_bn_apply pass over h), its backward finishes
+// the BN sums and goes straight on to the weight gradient (it was a mask launch with fp64 atomics plus a
+// weight-gradient launch re-folding them), and every weight-gradient column is complete inside one workgroup
+// (one writer, no split-K partials, deterministic).  The decoder-input forward recomputes the
+// reparameterisation of the whole batch (n x 2d latents, Philox + one exp each) in every workgroup instead of
+// reading a z that a separate launch would have to produce first; workgroup b stores its share of z.
+//
+// Arithmetic on v_mfma_f32_16x16x4_f32: the small operand (z, dheads: n x K, K <= 128) is staged in LDS at
+// pitch KR + 4 (zero-padded to KR columns and 16-row tiles), the workgroup's 16 weight columns are B fragments
+// in registers, and each wave walks 16-row tiles.  A fragment read is one ds_read_b128 of 4 consecutive k that
+// feed 4 MFMAs (step s of a 16-k chunk contracts k = 4 (lane / 16) + s on both operands).  The weight gradients
+// reuse the tile's output registers directly as the batch-side MFMA operand: lane l holds rows 4 (l / 16) + r,
+// column l % 16 of a 16x16 tile, which is exactly the (k = l / 16, column l % 16) fragment of step s = r.
+// Batch sums are accumulated in fp64 per lane and combined in a fixed order.
+#include <type_traits>
+#include "cv_common.hpp"
+
+namespace cv {
+namespace dl {
+
+constexpr int NTD = 256;
+constexpr int DF = 16;          // storage columns per workgroup
+constexpr int ZMAX = 16384;     // latents staged in LDS (n * KR)
+
+__device__ __forceinline__ int feature_of(int col, int pix, int ch) {  // PyTorch feature c*pix + p
+  if (pix <= 1) return col;
+  const int p = col / ch;
+  return (col - p * ch) * pix + p;
+}
+
+__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// dst[row][KR + 4] <- src[row][K] for rows < nt*16 (zero outside [n) x [K)); 16 loads in flight per thread
+template <int KR>
+__device__ __forceinline__ void stage_pad(const float* __restrict__ src, int n, int K, float* dst) {
+  constexpr int U = 16, P = KR + 4;
+  const long total = (long)((n + 15) & ~15) * KR;
+  for (long e0 = threadIdx.x; e0 < total; e0 += (long)NTD * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long e = e0 + (long)NTD * u;
+      const int row = (int)(e / KR), j = (int)(e % KR);
+      v[u] = (e < total && row < n && j < K) ? src[(size_t)row * K + j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long e = e0 + (long)NTD * u;
+      if (e >= total) break;
+      dst[(e / KR) * P + e % KR] = v[u];
+    }
+  }
+}
+
+// C (16 x 16) = A[row0 .. row0 + 16)[0 .. KR) (LDS, pitch KR + 4) x B (b: this lane's B fragments,
+// b[c][s] = B[16 c + 4 (lane / 16) + s][lane % 16]); lane l receives C[4 (l / 16) + r][l % 16] in [r]
+template <int KR>
+__device__ __forceinline__ f32x4 mma_rows(const float* sA, int row0, const f32x4* b) {
+  const int l = threadIdx.x & 63;
+  const float* a = sA + (row0 + (l & 15)) * (KR + 4) + 4 * (l >> 4);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < KR / 16; ++c) {
+    const f32x4 av = lds4(a + 16 * c);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], b[c][s], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// acc[jt] (16 x 16 tiles jt) += S[rows][jt*16 + i]^T (LDS, pitch KR + 4) x V[rows][lane column], rows = the 16 rows
+// of the tile at row0, V = this lane's tile registers (v[r] = row 4 (lane / 16) + r): lane l receives
+// [i = 4 (l / 16) + r][column l % 16]
+template <int KR>
+__device__ __forceinline__ void mma_rows_t(const float* sS, int row0, f32x4 v, f32x4* acc) {
+  const int l = threadIdx.x & 63;
+  const float* a = sS + (row0 + 4 * (l >> 4)) * (KR + 4) + (l & 15);
+#pragma unroll
+  for (int jt = 0; jt < KR / 16; ++jt)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s * (KR + 4) + 16 * jt], v[s], acc[jt], 0, 0, 0);
+}
+
+// fold a per-lane value over the 4 lanes of a column (l, l^16, l^32, l^48)
+template <class T>
+__device__ __forceinline__ T col_fold(T v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+struct FwdArgs {
+  const float* heads;   // [n][4d] (mu_c | lv_c | mu_s | lv_s); nullptr: z is an input
+  const float* eps;     // injected noise [n][2d] (test hook) or nullptr: Philox(seed, offset[0])
+  uint64_t seed;
+  uint64_t* offset;     // device (counter, arrival word); advanced once per launch (nullptr: none)
+  float* z;             // [n][2d]
+  const float* w;       // Linear weight [F][K], K = 2d
+  const float* bias;    // [F]
+  cv_bn bn;             // BatchNorm1d (train: batch statistics of h; eval: running statistics)
+  double* stat_out;     // train: the complete sums (sum h, sum h^2) go to replica 0 of [REPL][2][F]
+  float* h;             // [n][F] storage order (Linear output = BN input)
+  float* ah;            // [n][F] storage order (ReLU output)
+  int n, d, F, pix, ch;
+};
+
+// KR: K = 2d rounded up to a multiple of 16
+template <int KR>
+__global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int P = KR + 4;
+  const int K = 2 * A.d, n = A.n, F = A.F, nt = (n + 15) >> 4;
+  float* sz = smem;  // [nt * 16][P]
+  __shared__ double red[2][NTD / 64][DF];
+  __shared__ BnFwdC kf[DF];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
+  const int col0 = blockIdx.x * DF, col = col0 + lr;
+  const int f = feature_of(col, A.pix, A.ch);
+  const uint64_t off = A.offset ? A.offset[0] : 0;
+  // ---- latents: z = mu + eps * exp(lv / 2) (the arithmetic of reparam_kernel, element for element); every
+  // global load of a batch is issued before the first use
+  if (A.heads) {
+    const int d = A.d;
+    for (long e = t; e < (long)nt * 16 * KR; e += NTD) {  // the zero padding (disjoint from the latents)
+      const int row = (int)(e / KR), j = (int)(e % KR);
+      if (row >= n || j >= K) sz[row * P + j] = 0.f;
+    }
+    const long npair = (long)n * K / 2;  // (K even: a pair never straddles a row)
+    constexpr int U = 8;
+    for (long p0 = t; p0 < npair; p0 += (long)NTD * U) {
+      float2 mu[U], lv[U], ep[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = p0 + (long)NTD * u;
+        const long e = 2 * (p < npair ? p : 0);
+        const int row = (int)(e / K), j = (int)(e - (long)row * K);
+        const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
+        const float* hr = A.heads + (size_t)row * 4 * d;
+        mu[u] = make_float2(hr[blk * d + k], hr[blk * d + k + 1]);
+        lv[u] = make_float2(hr[(blk + 1) * d + k], hr[(blk + 1) * d + k + 1]);
+        if (A.eps) ep[u] = make_float2(A.eps[e], A.eps[e + 1]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = p0 + (long)NTD * u;
+        if (p >= npair) break;
+        if (!A.eps) normal2(A.seed, off, (uint64_t)p, ep[u].x, ep[u].y);
+        const long e = 2 * p;
+        const int row = (int)(e / K), j = (int)(e - (long)row * K);
+        const float v0 = mu[u].x + ep[u].x * expf(0.5f * lv[u].x);
+        const float v1 = mu[u].y + ep[u].y * expf(0.5f * lv[u].y);
+        sz[row * P + j] = v0;
+        sz[row * P + j + 1] = v1;
+        if ((int)((p >> 6) % gridDim.x) == (int)blockIdx.x) {  // this workgroup's share of z
+          A.z[e] = v0;
+          A.z[e + 1] = v1;
+        }
+      }
+    }
+  } else {
+    stage_pad<KR>(A.z, n, K, sz);
+  }
+  // ---- B fragments: W[f][k] (k = 16 c + 4 lq + s), and the bias
+  f32x4 b[KR / 16];
+#pragma unroll
+  for (int c = 0; c < KR / 16; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 16 * c + 4 * lq + s;
+      b[c][s] = k < K ? A.w[(size_t)f * K + k] : 0.f;
+    }
+  const float bv = A.bias ? A.bias[f] : 0.f;
+  __syncthreads();
+  // ---- pass 1: h and its batch sums
+  double s1 = 0.0, s2 = 0.0;
+  for (int tile = w; tile < nt; tile += NTD / 64) {
+    const f32x4 acc = mma_rows<KR>(sz, 16 * tile, b);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * tile + 4 * lq + r;
+      if (row >= n) continue;
+      const float v = acc[r] + bv;
+      A.h[(size_t)row * F + col] = v;
+      s1 += (double)v;
+      s2 += (double)v * (double)v;
+    }
+  }
+  const bool train = A.bn.train != 0;
+  s1 = col_fold(s1);
+  s2 = col_fold(s2);
+  if (lq == 0) {
+    red[0][w][lr] = s1;
+    red[1][w][lr] = s2;
+  }
+  __syncthreads();
+  if (t < DF) {
+    const int fc = feature_of(col0 + t, A.pix, A.ch);
+    double S = 0.0, Q = 0.0;
+    if (train) {
+#pragma unroll
+      for (int ww = 0; ww < NTD / 64; ++ww) {
+        S += red[0][ww][t];
+        Q += red[1][ww][t];
+      }
+      if (A.stat_out) {
+        A.stat_out[fc] = S;
+        A.stat_out[F + fc] = Q;
+      }
+    }
+    kf[t] = bn_fwd_const_s(A.bn, fc, S, Q);
+  }
+  __syncthreads();
+  // ---- pass 2: ah = ReLU(BN(h)), h recomputed (same arithmetic, same bits)
+  const BnFwdC k = kf[lr];
+  for (int tile = w; tile < nt; tile += NTD / 64) {
+    const f32x4 acc = mma_rows<KR>(sz, 16 * tile, b);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * tile + 4 * lq + r;
+      if (row < n) A.ah[(size_t)row * F + col] = bn_relu(acc[r] + bv, k);
+    }
+  }
+  // ---- the last workgroup to finish advances the noise counter (every workgroup read it above)
+  if (A.offset) {
+    __syncthreads();
+    if (t == 0) {
+      const unsigned long long prev = atomicAdd((unsigned long long*)(A.offset + 1), 1ull);
+      if (prev == (unsigned long long)(gridDim.x - 1)) {
+        A.offset[0] = off + 1;
+        A.offset[1] = 0;
+      }
+    }
+  }
+}
+
+struct BwdArgs {
+  float* ga;            // [n][F] storage order: in d(ReLU output), out d(h) = BN1d-backward(mask * ga)
+  const float* h;       // [n][F] BN input
+  cv_bn bn;             // BatchNorm1d, train mode (forward sums in bn.stat)
+  double* gstat_out;    // the complete backward sums (sum dz, sum dz*xhat) go to replica 0 of [REPL][2][F]
+  const float* z;       // [n][K] the Linear's input
+  float* gw;            // [F][K] += dW
+  int n, K, F, pix, ch;
+};
+
+constexpr int TB = 4;  // 16-row tiles whose elementwise loads are in flight together (per wave)
+
+template <int KR>
+__global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int P = KR + 4;
+  const int K = A.K, n = A.n, F = A.F, nt = (n + 15) >> 4;
+  float* sz = smem;                    // [nt * 16][P]
+  float* sred = smem + nt * 16 * P;    // [4 waves][DF][KR]: the weight-gradient fold
+  __shared__ double red[2][NTD / 64][DF];
+  __shared__ double fs[2][DF];
+  __shared__ BnFwdC kf[DF];
+  __shared__ BnBwdC kb[DF];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
+  const int col0 = blockIdx.x * DF, col = col0 + lr;
+  stage_pad<KR>(A.z, n, K, sz);
+  if (t < DF) {  // forward constants of the workgroup's features (replica fold, one thread per feature)
+    const int fc = feature_of(col0 + t, A.pix, A.ch);
+    double s, q;
+    bn_sums(A.bn.stat, F, fc, s, q);
+    fs[0][t] = s;
+    fs[1][t] = q;
+    kf[t] = bn_fwd_const_s(A.bn, fc, s, q);
+  }
+  __syncthreads();
+  const BnFwdC k = kf[lr];
+  // this lane's elements: rows 16 tile + 4 lq + r of column col, tiles w, w + 4, ...
+  auto load = [&](int tile0, float (*hv)[4], float (*dv)[4]) {
+#pragma unroll
+    for (int i = 0; i < TB; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * (tile0 + 4 * i) + 4 * lq + r;
+        const size_t o = (size_t)(row < n ? row : 0) * F + col;
+        hv[i][r] = A.h[o];
+        dv[i][r] = A.ga[o];
+      }
+  };
+  // ---- pass 1: ReLU mask, backward sums
+  double s1 = 0.0, s2 = 0.0;
+  for (int tile0 = w; tile0 < nt; tile0 += 4 * TB) {
+    float hv[TB][4], dv[TB][4];
+    load(tile0, hv, dv);
+#pragma unroll
+    for (int i = 0; i < TB; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * (tile0 + 4 * i) + 4 * lq + r;
+        if (row >= n) continue;
+        const float dm = bn_out(hv[i][r], k) <= 0.f ? 0.f : dv[i][r];
+        s1 += (double)dm;
+        s2 += (double)(dm * ((hv[i][r] - k.mu) * k.istd));
+      }
+  }
+  s1 = col_fold(s1);
+  s2 = col_fold(s2);
+  if (lq == 0) {
+    red[0][w][lr] = s1;
+    red[1][w][lr] = s2;
+  }
+  __syncthreads();
+  if (t < DF) {
+    const int fc = feature_of(col0 + t, A.pix, A.ch);
+    double G1 = 0.0, G2 = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < NTD / 64; ++ww) {
+      G1 += red[0][ww][t];
+      G2 += red[1][ww][t];
+    }
+    if (A.gstat_out) {
+      A.gstat_out[fc] = G1;
+      A.gstat_out[F + fc] = G2;
+    }
+    kb[t] = bn_bwd_const_s(A.bn, fc, fs[0][t], fs[1][t], G1, G2);
+  }
+  __syncthreads();
+  // ---- pass 2: d(h) written in place; dW[col][k] += sum_rows d(h)[row][col] z[row][k] on the MFMA pipe
+  const BnBwdC bb = kb[lr];
+  f32x4 acc[KR / 16];
+#pragma unroll
+  for (int j = 0; j < KR / 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tile0 = w; tile0 < nt; tile0 += 4 * TB) {
+    float hv[TB][4], dv[TB][4];
+    load(tile0, hv, dv);
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int tile = tile0 + 4 * i;
+      if (tile >= nt) break;
+      f32x4 dp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * tile + 4 * lq + r;
+        const float dm = bn_out(hv[i][r], k) <= 0.f ? 0.f : dv[i][r];
+        dp[r] = row < n ? bn_bwd(dm, hv[i][r], bb) : 0.f;
+        if (row < n) A.ga[(size_t)row * F + col] = dp[r];
+      }
+      // dW^T tile: [k][col] += z[rows][k]^T d(h)[rows][col]
+      mma_rows_t<KR>(sz, 16 * tile, dp, acc);
+    }
+  }
+  // lane l holds dW[col lr][k = 16 jt + 4 lq + r]: fold the 4 waves in order
+#pragma unroll
+  for (int jt = 0; jt < KR / 16; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sred[(w * DF + lr) * KR + 16 * jt + 4 * lq + r] = acc[jt][r];
+  __syncthreads();
+  for (int e = t; e < DF * K; e += NTD) {
+    const int cl = e / K, kk = e - cl * K;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NTD / 64; ++ww) v += sred[(ww * DF + cl) * KR + kk];
+    A.gw[(size_t)feature_of(col0 + cl, A.pix, A.ch) * K + kk] += v;
+  }
+}
+
+// ---------------------------------------------------------------- encoder heads backward
+struct HeadsArgs {
+  const float* dheads;  // [n][J], J = 4d
+  const float* w;       // [J][F] PyTorch feature order
+  const float* y;       // [n][F] storage order: the last encoder block's BN input
+  cv_bn bn;             // that BatchNorm2d (C channels, pix pixels per channel)
+  float* gin;           // [n][F] storage order: d(BN output) = (dheads W) * [ReLU active]
+  double* gstat_out;    // [REPL][2][C] backward sums (+=)
+  float* gw;            // [J][F] +=
+  float* gb;            // [J] += (workgroup 0)
+  int n, J, F, pix, ch;
+};
+
+template <int JR>
+__global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int P = JR + 4;
+  const int J = A.J, n = A.n, F = A.F, C = A.ch, nt = (n + 15) >> 4;
+  float* sd = smem;  // [nt * 16][P]; after the tiles: the weight-gradient fold, then the finalisation scratch
+  __shared__ BnFwdC kf[DF];
+  __shared__ double red[2][NTD / 64][DF];
+  __shared__ int flag;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
+  const int col0 = blockIdx.x * DF, col = col0 + lr;
+  const int f = feature_of(col, A.pix, C);
+  stage_pad<JR>(A.dheads, n, J, sd);
+  f32x4 b[JR / 16];  // B fragments: W[j][f], j = 16 c + 4 lq + s
+#pragma unroll
+  for (int c = 0; c < JR / 16; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int j = 16 * c + 4 * lq + s;
+      b[c][s] = j < J ? A.w[(size_t)j * F + f] : 0.f;
+    }
+  if (t < DF) {  // the layer's forward constants: finalised by its producer, or folded from the replicas
+    const int cc = (col0 + t) % C;
+    const cv_bn& bn = A.bn;
+    if (bn.train && bn.cfwd && bn.ticket && bn.ticket[0] != 0u)
+      kf[t] = BnFwdC{bn.cfwd[cc], bn.cfwd[C + cc], bn.cfwd[2 * C + cc], bn.cfwd[3 * C + cc]};
+    else
+      kf[t] = bn_fwd_const(bn, cc);
+  }
+  __syncthreads();
+  const BnFwdC k = kf[lr];
+  f32x4 acc[JR / 16];
+#pragma unroll
+  for (int j = 0; j < JR / 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double s1 = 0.0, s2 = 0.0;
+  for (int tile0 = w; tile0 < nt; tile0 += 4 * TB) {
+    float yv[TB][4];
+#pragma unroll
+    for (int i = 0; i < TB; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * (tile0 + 4 * i) + 4 * lq + r;
+        yv[i][r] = A.y[(size_t)(row < n ? row : 0) * F + col];
+      }
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int tile = tile0 + 4 * i;
+      if (tile >= nt) break;
+      const f32x4 g = mma_rows<JR>(sd, 16 * tile, b);
+      f32x4 a;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * tile + 4 * lq + r;
+        const float o = bn_out(yv[i][r], k);
+        const float dz = o > 0.f ? g[r] : 0.f;
+        a[r] = row < n ? fmaxf(o, 0.f) : 0.f;
+        if (row < n) {
+          A.gin[(size_t)row * F + col] = dz;
+          s1 += (double)dz;
+          s2 += (double)(dz * ((yv[i][r] - k.mu) * k.istd));
+        }
+      }
+      // dW tile: [j][col] += dheads[rows][j]^T ReLU(BN(y))[rows][col]
+      mma_rows_t<JR>(sd, 16 * tile, a, acc);
+    }
+  }
+  // head biases: workgroup 0, one thread per head output
+  if (blockIdx.x == 0 && A.gb) {
+    for (int j = t; j < J; j += NTD) {
+      float v = 0.f;
+      for (int r = 0; r < n; ++r) v += sd[r * P + j];
+      A.gb[j] += v;
+    }
+  }
+  s1 = col_fold(s1);
+  s2 = col_fold(s2);
+  if (lq == 0) {
+    red[0][w][lr] = s1;
+    red[1][w][lr] = s2;
+  }
+  __syncthreads();  // (every wave is done with sd: it becomes the fold area)
+  float* sred = smem;  // [4 waves][JR][DF]
+#pragma unroll
+  for (int jt = 0; jt < JR / 16; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sred[(w * JR + 16 * jt + 4 * lq + r) * DF + lr] = acc[jt][r];
+  if (t < DF && A.gstat_out) {
+    double a = 0.0, q = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < NTD / 64; ++ww) {
+      a += red[0][ww][t];
+      q += red[1][ww][t];
+    }
+    const int cc = (col0 + t) % C;
+    const int repl = blockIdx.x % CV_STAT_REPL(C);
+    atomic_add_f64(A.gstat_out + (size_t)repl * 2 * C + cc, a);
+    atomic_add_f64(A.gstat_out + (size_t)repl * 2 * C + C + cc, q);
+  }
+  __syncthreads();
+  for (int e = t; e < J * DF; e += NTD) {  // e = j * DF + column: 16 consecutive columns per head output
+    const int j = e / DF, cl = e - j * DF;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NTD / 64; ++ww) v += sred[(ww * JR + j) * DF + cl];
+    A.gw[(size_t)j * F + feature_of(col0 + cl, A.pix, C)] += v;
+  }
+  __syncthreads();  // (the fold area becomes the finalisation scratch)
+  if (A.gstat_out) bn_finalize<NTD>(A.bn, A.gstat_out, true, reinterpret_cast<double*>(smem), &flag);
+}
+
+template <class Fn>
+static int pick_kr(int K, Fn fn) {
+  if (K <= 16) return fn(std::integral_constant<int, 16>());
+  if (K <= 32) return fn(std::integral_constant<int, 32>());
+  if (K <= 64) return fn(std::integral_constant<int, 64>());
+  if (K <= 128) return fn(std::integral_constant<int, 128>());
+  return -1;
+}
+
+static int set_lds(const void* kern, size_t bytes) {
+  if (bytes <= 64 * 1024) return 0;
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace dl
+}  // namespace cv
+
+using namespace cv;
+using namespace cv::dl;
+
+extern "C" int cv_decoder_input_supported(int n, int d, int features) {
+  const int K = 2 * d;
+  const int KR = K <= 16 ? 16 : K <= 32 ? 32 : K <= 64 ? 64 : 128;
+  return (n >= 1 && d >= 1 && K <= 128 && (long)((n + 15) & ~15) * KR <= ZMAX && features % DF == 0) ? 1 : 0;
+}
+
+extern "C" int cv_decoder_input_forward(const cv_linear* g, const float* heads, const float* eps, uint64_t seed,
+                                        uint64_t* offset, float* z, const float* weight, const float* bias,
+                                        const cv_bn* bn, double* stat_out, float* h, float* ah, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(g && z && weight && bn && h && ah, "decoder_input_forward: null args");
+  CV_REQUIRE(g->in_features % 2 == 0 && g->out_features == bn->C, "decoder_input_forward: bad shapes");
+  const int d = g->in_features / 2, F = g->out_features;
+  CV_REQUIRE(cv_decoder_input_supported(g->n, d, F), "decoder_input_forward: n=%d, K=%d, F=%d outside the fused "
+             "contract (n*K <= %d, K <= 128, F %% %d == 0)", g->n, 2 * d, F, ZMAX, DF);
+  CV_REQUIRE(!heads || eps || offset, "decoder_input_forward: need injected eps or a device offset counter");
+  const int pix = g->out_pix > 0 ? g->out_pix : 1, ch = g->out_ch;
+  CV_REQUIRE(pix <= 1 || pix * ch == F, "decoder_input_forward: out_pix*out_ch != out_features");
+  FwdArgs a;
+  a.heads = heads;
+  a.eps = eps;
+  a.seed = seed;
+  a.offset = heads ? offset : nullptr;
+  a.z = z;
+  a.w = weight;
+  a.bias = bias;
+  a.bn = *bn;
+  a.stat_out = bn->train ? stat_out : nullptr;
+  a.h = h;
+  a.ah = ah;
+  a.n = g->n;
+  a.d = d;
+  a.F = F;
+  a.pix = pix;
+  a.ch = ch;
+  return pick_kr(2 * d, [&](auto kr) -> int {
+    constexpr int KR = decltype(kr)::value;
+    const size_t lds = (size_t)((g->n + 15) & ~15) * (KR + 4) * sizeof(float);
+    const void* kern = (const void*)declinear_fwd_kernel<KR>;
+    if (set_lds(kern, lds)) {
+      set_error("decoder_input_forward: LDS carve-out of %zu bytes refused", lds);
+      return 1;
+    }
+    hipLaunchKernelGGL(declinear_fwd_kernel<KR>, dim3(F / DF), dim3(NTD), lds, S(stream), a);
+    CV_LAUNCH_CHECK("decoder_input_forward");
+    return 0;
+  });
+}
+
+extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const float* h, const cv_bn* bn,
+                                         double* gstat_out, const float* z, float* gweight, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(g && ga && h && bn && z && gweight, "decoder_input_backward: null args");
+  CV_REQUIRE(bn->train && bn->stat && g->out_features == bn->C && g->in_features % 2 == 0,
+             "decoder_input_backward: BN1d must be train-mode with its forward sums, C = out_features");
+  const int K = g->in_features, F = g->out_features;
+  CV_REQUIRE(cv_decoder_input_supported(g->n, K / 2, F), "decoder_input_backward: outside the fused contract");
+  const int pix = g->out_pix > 0 ? g->out_pix : 1;
+  BwdArgs a;
+  a.ga = ga;
+  a.h = h;
+  a.bn = *bn;
+  a.gstat_out = gstat_out;
+  a.z = z;
+  a.gw = gweight;
+  a.n = g->n;
+  a.K = K;
+  a.F = F;
+  a.pix = pix;
+  a.ch = g->out_ch;
+  return pick_kr(K, [&](auto kr) -> int {
+    constexpr int KR = decltype(kr)::value;
+    const size_t lds = ((size_t)((g->n + 15) & ~15) * (KR + 4) + (size_t)(NTD / 64) * DF * KR) * sizeof(float);
+    const void* kern = (const void*)declinear_bwd_kernel<KR>;
+    if (set_lds(kern, lds)) {
+      set_error("decoder_input_backward: LDS carve-out of %zu bytes refused", lds);
+      return 1;
+    }
+    hipLaunchKernelGGL(declinear_bwd_kernel<KR>, dim3(F / DF), dim3(NTD), lds, S(stream), a);
+    CV_LAUNCH_CHECK("decoder_input_backward");
+    return 0;
+  });
+}
+
+static size_t heads_lds(int n, int J) {
+  const int JR = J <= 32 ? 32 : J <= 64 ? 64 : 128;
+  size_t a = (size_t)((n + 15) & ~15) * (JR + 4) * sizeof(float);
+  const size_t fold = (size_t)(NTD / 64) * DF * 128 * sizeof(float), fin = 4 * NTD * sizeof(double);
+  if (a < fold) a = fold;
+  if (a < fin) a = fin;
+  return a;
+}
+
+extern "C" int cv_heads_backward_supported(int n, int in_features, int in_ch, int out_features) {
+  return (n >= 1 && out_features >= 1 && out_features <= 128 && in_features % DF == 0 && in_ch % DF == 0 &&
+          heads_lds(n, out_features) <= 150 * 1024) ? 1 : 0;
+}
+
+extern "C" int cv_heads_backward(const cv_linear* g, const float* dheads, const float* weight, const float* y,
+                                 const cv_bn* bn, float* gin, double* gstat_out, float* gweight, float* gbias,
+                                 cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(g && dheads && weight && y && bn && gin && gweight, "heads_backward: null args");
+  const int pix = g->in_pix > 0 ? g->in_pix : 1, ch = pix > 1 ? g->in_ch : g->in_features;
+  CV_REQUIRE(pix * ch == g->in_features && bn->C == ch, "heads_backward: in_pix*in_ch != in_features or BN C != in_ch");
+  CV_REQUIRE(cv_heads_backward_supported(g->n, g->in_features, ch, g->out_features),
+             "heads_backward: n=%d, out_features=%d outside the fused contract", g->n, g->out_features);
+  HeadsArgs a;
+  a.dheads = dheads;
+  a.w = weight;
+  a.y = y;
+  a.bn = *bn;
+  a.gin = gin;
+  a.gstat_out = gstat_out;
+  a.gw = gweight;
+  a.gb = gbias;
+  a.n = g->n;
+  a.J = g->out_features;
+  a.F = g->in_features;
+  a.pix = pix;
+  a.ch = ch;
+  const size_t lds = heads_lds(g->n, a.J);
+  auto go = [&](auto jr) -> int {
+    constexpr int JR = decltype(jr)::value;
+    const void* kern = (const void*)heads_bwd_kernel<JR>;
+    if (set_lds(kern, lds)) {
+      set_error("heads_backward: LDS carve-out of %zu bytes refused", lds);
+      return 1;
+    }
+    hipLaunchKernelGGL(heads_bwd_kernel<JR>, dim3(a.F / DF), dim3(NTD), lds, S(stream), a);
+    CV_LAUNCH_CHECK("heads_backward");
+    return 0;
+  };
+  if (a.J <= 32) return go(std::integral_constant<int, 32>());
+  if (a.J <= 64) return go(std::integral_constant<int, 64>());
+  return go(std::integral_constant<int, 128>());
+}

@@ -196,6 +196,21 @@ _SIGS = {
         c_int,
         [_P(cv_linear), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "cv_decoder_input_supported": (c_int, [c_int, c_int, c_int]),
+    "cv_decoder_input_forward": (
+        c_int,
+        [_P(cv_linear), c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, _P(cv_bn), c_void_p,
+         c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_decoder_input_backward": (
+        c_int,
+        [_P(cv_linear), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "cv_heads_backward_supported": (c_int, [c_int, c_int, c_int, c_int]),
+    "cv_heads_backward": (
+        c_int,
+        [_P(cv_linear), c_void_p, c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "cv_bn_apply": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cv_bn_update_running": (c_int, [_P(cv_bn), c_int, c_float, _P(c_void_p), c_void_p]),
     "cv_bn_batch_stats": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_void_p]),

@@ -321,8 +321,8 @@ class ClearStep:
                 ws.decoder_program(f, ws.z, True, "loss", X, rec_scale=gscale_rec)
                 f.keep += [gwork, gscale_rec]
             else:
-                ws.reparam_program(f, eps_buf[0] if inject else None, self.seed, self.offset)
-                ws.decoder_program(f, ws.z, True, "loss", X)
+                ws.decoder_program(f, ws.z, True, "loss", X,
+                                   reparam=(eps_buf[0] if inject else None, self.seed, self.offset))
             # (the running statistics are folded at the end of the backward by cv_step_reduce)
             return f
 
@@ -433,14 +433,13 @@ class ClearStep:
                 else:
                     prog.add("cv_zero_many", ptr_array([ws.dec_stats.data_ptr(), ws.dec_tickets.data_ptr()]),
                              (ctypes.c_size_t * 2)(ws.dec_stats.numel() * 8, ws.dec_tickets.numel() * 8), 2)
-                ws.reparam_program(prog, eps_buf[1 + j] if inject else None, self.seed, self.offset)
+                return (eps_buf[1 + j] if inject else None, self.seed, self.offset)
 
             def make_learn(inject: bool):
                 lp = Program()
                 pack_program(sp, lp, "all")  # the VAE Adam step just moved the weights
                 for j in range(5):
-                    learn_forward(lp, j, inject)
-                    ws.decoder_program(lp, ws.z, True, "none")
+                    ws.decoder_program(lp, ws.z, True, "none", reparam=learn_forward(lp, j, inject))
                     ws.running_program(lp, "all")
                     lp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
                            self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
@@ -455,8 +454,7 @@ class ClearStep:
                     gp = Program()
                     if j == 0:
                         pack_program(sp, gp, "all")
-                    learn_forward(gp, j, inject)
-                    ws.decoder_program(gp, ws.z, True, "none")
+                    ws.decoder_program(gp, ws.z, True, "none", reparam=learn_forward(gp, j, inject))
                     ws.running_program(gp, "all")
                     gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
                            self.learn.data_ptr() + 4 * j, G, None, None, None, None, 0, None, None)
@@ -482,8 +480,8 @@ class ClearStep:
                 pack_program(sp, gp, "all")  # the VAE Adam step just moved the weights
                 gp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
                 ws.encoder_program(gp, X, True)
-                ws.reparam_program(gp, eps_buf[1] if inject else None, self.seed, self.offset)
-                ws.decoder_program(gp, ws.z, True, "none")
+                ws.decoder_program(gp, ws.z, True, "none",
+                                   reparam=(eps_buf[1] if inject else None, self.seed, self.offset))
                 ws.running_program(gp, "all")
                 gp.add("cv_tc_learning_step", disc, ws.z, n, tc_work, self.learn, G)
                 ap = Program()

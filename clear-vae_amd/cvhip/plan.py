@@ -649,8 +649,7 @@ class Workspace:
         if train:
             P.add("cv_zero", self.stats, self.stats.numel() * 8)
         self.encoder_program(P, x, train)
-        self.reparam_program(P, eps, seed, offset)
-        self.decoder_program(P, self.z, train, output, x, rec_scale)
+        self.decoder_program(P, self.z, train, output, x, rec_scale, reparam=(eps, seed, offset))
         if train:
             self.running_program(P, "all")
         return P
@@ -687,13 +686,43 @@ class Workspace:
         (P.add_side if side else P.add)("cv_bn_update_running", bns, len(views),
                                         ctypes.c_float(float(views[0].mod.momentum)), nbt)
 
-    def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None):
+    # cv_decoder_input_forward / _backward (cv_declinear.hip): the reparameterisation, the decoder Linear, its
+    # BatchNorm1d and ReLU in one launch, and the mask + BN1d backward + Linear weight gradient in one launch
+    # (CVHIP_FUSED_DECIN=0: the separate reparam / Linear / bn_apply and mask / weight-gradient launches)
+    FUSED_DECIN = os.environ.get("CVHIP_FUSED_DECIN", "1") != "0"
+
+    def fused_decoder_input(self) -> bool:
+        sp = self.spec
+        return self.FUSED_DECIN and bool(_lib.lib().cv_decoder_input_supported(self.n, sp.d, sp.dec_lin.out_features))
+
+    # cv_heads_backward (cv_declinear.hip): the heads' data and weight gradients with the last encoder block's
+    # ReLU mask and BN backward sums in one launch (CVHIP_FUSED_HEADS=0: the DENSE backward-data GEMM and the
+    # deferred split-K weight gradient)
+    FUSED_HEADS = os.environ.get("CVHIP_FUSED_HEADS", "1") != "0"
+
+    def fused_heads(self) -> bool:
+        sp = self.spec
+        C, Hh, Wh = sp.feat
+        return self.FUSED_HEADS and bool(_lib.lib().cv_heads_backward_supported(self.n, sp.F, C, 4 * sp.d))
+
+    def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None):
+        """reparam = (eps, seed, offset): z is drawn from self.heads first (cv_reparam_forward, or inside the
+        fused decoder-input launch); None: z is given."""
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
-        ep = ep_fwd(self.bn_1d) if train else ep_none()
-        P.add("cv_linear_forward", lin, operand(z), sp.dec_lin.weight, sp.dec_lin.bias, self.h, 0, ep)
-        P.add("cv_bn_apply", self.bn_1d.cv(train), self.h, self.ah, n, sp.dec_lin.out_features, Hu * Wu, Cu, 1)
+        if self.fused_decoder_input():
+            eps, seed, offset = reparam if reparam is not None else (None, 0, None)
+            P.add("cv_decoder_input_forward", lin, self.heads if reparam is not None else None,
+                  eps.data_ptr() if eps is not None else None, ctypes.c_uint64(seed),
+                  offset.data_ptr() if offset is not None else None, z, sp.dec_lin.weight, sp.dec_lin.bias,
+                  self.bn_1d.cv(train), self.bn_1d.stat if train else None, self.h, self.ah)
+        else:
+            if reparam is not None:
+                self.reparam_program(P, *reparam)
+            ep = ep_fwd(self.bn_1d) if train else ep_none()
+            P.add("cv_linear_forward", lin, operand(z), sp.dec_lin.weight, sp.dec_lin.bias, self.h, 0, ep)
+            P.add("cv_bn_apply", self.bn_1d.cv(train), self.h, self.ah, n, sp.dec_lin.out_features, Hu * Wu, Cu, 1)
         cur = self.ah
         for li, c in enumerate(sp.dec):
             g = c.geom(n)
@@ -729,11 +758,16 @@ class Workspace:
             self._wgrad_call(P, "conv", g, xin, gout, param_grad(c.mod.weight), None, ("dec", li), defer)
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
-        P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
-              self.z, param_grad(sp.dec_lin.weight))
+        if self.fused_decoder_input():  # gah <- d(h) in place, weight gradient, BN1d backward sums
+            P.add("cv_decoder_input_backward", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
+                  self.z, param_grad(sp.dec_lin.weight))
+            gout = operand(self.gah)
+        else:
+            P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
+                  self.z, param_grad(sp.dec_lin.weight))
+            gout = operand(self.gah, XF_BNBWD, self.bn_1d.cv(True), y=self.h)
         if zero_dz:  # (else the caller zeroed it earlier in the step)
             P.add("cv_zero", dz_out, dz_out.numel() * 4)
-        gout = operand(self.gah, XF_BNBWD, self.bn_1d.cv(True), y=self.h)
         P.add("cv_linear_backward_data", lin, gout, sp.dec_lin.weight, dz_out, 1, ep_none())
 
     def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None, defer=None, heads=True,
@@ -743,7 +777,11 @@ class Workspace:
         backward order, for the second) so the first part's gradient bucket is reduced during the second."""
         sp, n = self.spec, self.n
         C, Hh, Wh = sp.feat
-        if heads:
+        if heads and self.fused_heads():
+            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
+            P.add("cv_heads_backward", lin, dheads, sp.heads[0].weight, self.y_enc[-1], self.bn_enc[-1].cv(True),
+                  self.g_enc[-1], self.bn_enc[-1].gstat, param_grad(sp.heads[0].weight), param_grad(sp.heads[0].bias))
+        elif heads:
             lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
             a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
             self._wgrad_call(P, "linear", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),

@@ -201,6 +201,37 @@ int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, 
                                  double* gstat_out, const float* zin, float* gweight,
                                  cv_stream_t stream);
 
+/* The decoder's input block in one launch each way (cv_declinear.hip): a workgroup owns 16 features of the
+ * [n][out_features] activation for the whole batch, so the BatchNorm1d statistics are complete inside it.
+ * Forward (VAE.sample vae.py:56-60, then decoder Linear -> BatchNorm1d -> ReLU vae.py:33-35): heads != NULL:
+ * z = mu + eps*exp(lv/2) from heads [n][4d] exactly as cv_reparam_forward (eps injected, or Philox(seed,
+ * offset[0]) with offset advanced once), written to z; heads == NULL: z [n][2d] is the input.  h = Linear(z)
+ * (storage order out_pix/out_ch), ah = ReLU(BN1d(h)); train: the complete batch sums of h are written to
+ * replica 0 of stat_out [REPL][2][F] (the other replicas must be zero).  Replaces cv_reparam_forward +
+ * cv_linear_forward + cv_bn_apply.
+ * Backward (trainer.py:482 through vae.py:33-35): ga [n][F] = d(ReLU output) is overwritten with d(h) (ReLU
+ * mask, then the BN1d backward transform); gstat_out replica 0 receives the complete backward sums; gweight
+ * [F][2d] += d(h)^T z.  dz = d(h) W is left to cv_linear_backward_data (no transform).  Replaces the two
+ * launches of cv_declinear_backward_weight.  Contract: cv_decoder_input_supported(n, d, F) (n*2d <= 16384,
+ * 2d <= 128, F % 16 == 0). */
+int cv_decoder_input_supported(int n, int d, int features);
+int cv_decoder_input_forward(const cv_linear* g, const float* heads, const float* eps, uint64_t seed,
+                             uint64_t* offset, float* z, const float* weight, const float* bias, const cv_bn* bn,
+                             double* stat_out, float* h, float* ah, cv_stream_t stream);
+int cv_decoder_input_backward(const cv_linear* g, float* ga, const float* h, const cv_bn* bn, double* gstat_out,
+                              const float* z, float* gweight, cv_stream_t stream);
+
+/* Encoder heads backward in one launch (the four nn.Linear heads vae.py:27-30 as one [4d][F] weight over the
+ * Flatten of the last conv block, vae.py:25; trainer.py:482): gin [n][F] (storage order in_pix/in_ch) =
+ * (dheads W) * [BN(y) > 0] with that BatchNorm2d's backward sums added to gstat_out (fp64 replicas; the layer's
+ * cbwd constants are finalised by the last workgroup when bn carries a ticket), gweight [4d][F] +=
+ * dheads^T ReLU(BN(y)), gbias [4d] += column sums of dheads.  Replaces cv_linear_backward_data with a
+ * CV_STAT_BWD epilogue plus cv_linear_backward_weight(_deferred) of the heads.  Contract:
+ * cv_heads_backward_supported(n, in_features, in_ch, out_features) (4d <= 128, dheads staged in LDS). */
+int cv_heads_backward_supported(int n, int in_features, int in_ch, int out_features);
+int cv_heads_backward(const cv_linear* g, const float* dheads, const float* weight, const float* y, const cv_bn* bn,
+                      float* gin, double* gstat_out, float* gweight, float* gbias, cv_stream_t stream);
+
 /* out = max(BN(x), 0) elementwise for a BatchNorm1d over `features` PyTorch-order features whose
  * tensor is stored in the Unflatten/NHWC order (pix, ch) (vae.py:34-36); rows = batch. */
 int cv_bn_apply(const cv_bn* bn, const float* x, float* out, int rows, int features, int pix, int ch,

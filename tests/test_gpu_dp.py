@@ -23,7 +23,7 @@ import pytest
 import torch
 
 import dp_gpu_worker
-from test_gpu_parity import LOSS_TOL, _bias_before_bn, _check_grads
+from test_gpu_parity import LOSS_TOL, _bias_before_bn, _check_grads, _conditioning
 
 pytestmark = pytest.mark.gpu
 
@@ -122,7 +122,15 @@ def test_dp_clear_step_world2(arch, n_global, precision):
     mean_g = {k: (shards[0]["grads"][k] + shards[1]["grads"][k]) / 2 for k in shards[0]["grads"]}
     got_g = {k: torch.tensor(v) for k, v in res[0]["grad"].items()}
     if precision == "fp32":
-        _check_grads(got_g, mean_g, arch)
+        # the averaged gradient's own sensitivity to an fp32-sized input perturbation (test_gpu_parity
+        # _conditioning): the VAE64 shard of 32 images sits near ReLU knife edges (median ~5e-4 run to run)
+        def step(xp):
+            outs = [R.clear_step(R.to_torch(sd), torch.tensor(xp[lo:hi]), torch.tensor(label[lo:hi]),
+                                 torch.tensor(ec[lo:hi]), torch.tensor(es[lo:hi]), arch, hp)
+                    for lo, hi in (res[0]["bounds"], res[1]["bounds"])]
+            return {"grads": {k: (outs[0]["grads"][k] + outs[1]["grads"][k]) / 2 for k in outs[0]["grads"]}}
+
+        _check_grads(got_g, mean_g, arch, floor=_conditioning({"grads": mean_g}, step, x))
         ref_p = _adam_ref(sd, mean_g, arch=arch)
         prel = sorted((_rel(res[0]["p1"][k], ref_p[k]), k) for k in ref_p)
         assert prel[len(prel) // 2][0] < 1e-5, prel[-3:]

@@ -68,7 +68,7 @@ def _check_grads(named_grads, ref_grads, arch, floor=(0.0, 0.0)):
         worst.append((_rel(g, g_ref), k))
     worst.sort(reverse=True)
     med = sorted(w for w, _ in worst)[len(worst) // 2]
-    assert med < max(5e-4, 2 * floor[0]), ("median per-tensor grad rel", med, floor)
+    assert med < max(5e-4, 2 * floor[0]), ("median per-tensor grad rel", med, floor, worst[:6])
     assert (num / den) ** 0.5 < max(2e-3, 2 * floor[1]), ("global grad rel", (num / den) ** 0.5, worst[:3], floor)
     assert worst[0][0] < 2e-2, worst[:3]
 
