@@ -28,8 +28,15 @@
 namespace cv {
 namespace dl {
 
-constexpr int NTD = 256;
+#ifndef CV_DL_NT
+#define CV_DL_NT 512
+#endif
+constexpr int NTD = CV_DL_NT;  // 8 waves: the workgroup is alone on its CU (128 of them), so its waves hide
+                               // each other's load latency and split the per-workgroup Philox draws
+                               // (256 / 512 / 1024 threads: MNIST forward 22.6 / 17.0 / 17.5 us, heads backward
+                               // 18.2 / 14.7 / 14.0 us; VAE64 forward 35.6 / 26.3 / 28.6 us)
 constexpr int DF = 16;          // storage columns per workgroup
+constexpr int NW = NTD / 64;    // waves
 constexpr int ZMAX = 16384;     // latents staged in LDS (n * KR)
 
 __device__ __forceinline__ int feature_of(int col, int pix, int ch) {  // PyTorch feature c*pix + p
@@ -128,6 +135,16 @@ __global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
   const int col0 = blockIdx.x * DF, col = col0 + lr;
   const int f = feature_of(col, A.pix, A.ch);
   const uint64_t off = A.offset ? A.offset[0] : 0;
+  // ---- B fragments: W[f][k] (k = 16 c + 4 lq + s), and the bias (requested first: used last)
+  f32x4 b[KR / 16];
+#pragma unroll
+  for (int c = 0; c < KR / 16; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 16 * c + 4 * lq + s;
+      b[c][s] = k < K ? A.w[(size_t)f * K + k] : 0.f;
+    }
+  const float bv = A.bias ? A.bias[f] : 0.f;
   // ---- latents: z = mu + eps * exp(lv / 2) (the arithmetic of reparam_kernel, element for element); every
   // global load of a batch is issued before the first use
   if (A.heads) {
@@ -147,9 +164,9 @@ __global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
         const int row = (int)(e / K), j = (int)(e - (long)row * K);
         const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
         const float* hr = A.heads + (size_t)row * 4 * d;
-        mu[u] = make_float2(hr[blk * d + k], hr[blk * d + k + 1]);
-        lv[u] = make_float2(hr[(blk + 1) * d + k], hr[(blk + 1) * d + k + 1]);
-        if (A.eps) ep[u] = make_float2(A.eps[e], A.eps[e + 1]);
+        mu[u] = *reinterpret_cast<const float2*>(hr + blk * d + k);  // (k even, d even: 8-byte aligned)
+        lv[u] = *reinterpret_cast<const float2*>(hr + (blk + 1) * d + k);
+        if (A.eps) ep[u] = *reinterpret_cast<const float2*>(A.eps + e);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -171,16 +188,6 @@ __global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
   } else {
     stage_pad<KR>(A.z, n, K, sz);
   }
-  // ---- B fragments: W[f][k] (k = 16 c + 4 lq + s), and the bias
-  f32x4 b[KR / 16];
-#pragma unroll
-  for (int c = 0; c < KR / 16; ++c)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = 16 * c + 4 * lq + s;
-      b[c][s] = k < K ? A.w[(size_t)f * K + k] : 0.f;
-    }
-  const float bv = A.bias ? A.bias[f] : 0.f;
   __syncthreads();
   // ---- pass 1: h and its batch sums
   double s1 = 0.0, s2 = 0.0;
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   constexpr int P = KR + 4;
   const int K = A.K, n = A.n, F = A.F, nt = (n + 15) >> 4;
   float* sz = smem;                    // [nt * 16][P]
-  float* sred = smem + nt * 16 * P;    // [4 waves][DF][KR]: the weight-gradient fold
+  float* sred = smem + nt * 16 * P;    // [NW waves][DF][KR]: the weight-gradient fold
   __shared__ double red[2][NTD / 64][DF];
   __shared__ double fs[2][DF];
   __shared__ BnFwdC kf[DF];
@@ -286,7 +293,7 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
     for (int i = 0; i < TB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * (tile0 + 4 * i) + 4 * lq + r;
+        const int row = 16 * (tile0 + NW * i) + 4 * lq + r;
         const size_t o = (size_t)(row < n ? row : 0) * F + col;
         hv[i][r] = A.h[o];
         dv[i][r] = A.ga[o];
@@ -294,14 +301,14 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   };
   // ---- pass 1: ReLU mask, backward sums
   double s1 = 0.0, s2 = 0.0;
-  for (int tile0 = w; tile0 < nt; tile0 += 4 * TB) {
+  for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
     float hv[TB][4], dv[TB][4];
     load(tile0, hv, dv);
 #pragma unroll
     for (int i = 0; i < TB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * (tile0 + 4 * i) + 4 * lq + r;
+        const int row = 16 * (tile0 + NW * i) + 4 * lq + r;
         if (row >= n) continue;
         const float dm = bn_out(hv[i][r], k) <= 0.f ? 0.f : dv[i][r];
         s1 += (double)dm;
@@ -335,12 +342,12 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   f32x4 acc[KR / 16];
 #pragma unroll
   for (int j = 0; j < KR / 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int tile0 = w; tile0 < nt; tile0 += 4 * TB) {
+  for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
     float hv[TB][4], dv[TB][4];
     load(tile0, hv, dv);
 #pragma unroll
     for (int i = 0; i < TB; ++i) {
-      const int tile = tile0 + 4 * i;
+      const int tile = tile0 + NW * i;
       if (tile >= nt) break;
       f32x4 dp;
 #pragma unroll
@@ -354,7 +361,7 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
       mma_rows_t<KR>(sz, 16 * tile, dp, acc);
     }
   }
-  // lane l holds dW[col lr][k = 16 jt + 4 lq + r]: fold the 4 waves in order
+  // lane l holds dW[col lr][k = 16 jt + 4 lq + r]: fold the waves in order
 #pragma unroll
   for (int jt = 0; jt < KR / 16; ++jt)
 #pragma unroll
@@ -394,7 +401,6 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
   const int col0 = blockIdx.x * DF, col = col0 + lr;
   const int f = feature_of(col, A.pix, C);
-  stage_pad<JR>(A.dheads, n, J, sd);
   f32x4 b[JR / 16];  // B fragments: W[j][f], j = 16 c + 4 lq + s
 #pragma unroll
   for (int c = 0; c < JR / 16; ++c)
@@ -403,6 +409,7 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
       const int j = 16 * c + 4 * lq + s;
       b[c][s] = j < J ? A.w[(size_t)j * F + f] : 0.f;
     }
+  stage_pad<JR>(A.dheads, n, J, sd);
   if (t < DF) {  // the layer's forward constants: finalised by its producer, or folded from the replicas
     const int cc = (col0 + t) % C;
     const cv_bn& bn = A.bn;
@@ -417,18 +424,18 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
 #pragma unroll
   for (int j = 0; j < JR / 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   double s1 = 0.0, s2 = 0.0;
-  for (int tile0 = w; tile0 < nt; tile0 += 4 * TB) {
+  for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
     float yv[TB][4];
 #pragma unroll
     for (int i = 0; i < TB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * (tile0 + 4 * i) + 4 * lq + r;
+        const int row = 16 * (tile0 + NW * i) + 4 * lq + r;
         yv[i][r] = A.y[(size_t)(row < n ? row : 0) * F + col];
       }
 #pragma unroll
     for (int i = 0; i < TB; ++i) {
-      const int tile = tile0 + 4 * i;
+      const int tile = tile0 + NW * i;
       if (tile >= nt) break;
       const f32x4 g = mma_rows<JR>(sd, 16 * tile, b);
       f32x4 a;
@@ -463,7 +470,7 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
     red[1][w][lr] = s2;
   }
   __syncthreads();  // (every wave is done with sd: it becomes the fold area)
-  float* sred = smem;  // [4 waves][JR][DF]
+  float* sred = smem;  // [NW waves][JR][DF]
 #pragma unroll
   for (int jt = 0; jt < JR / 16; ++jt)
 #pragma unroll
@@ -519,7 +526,9 @@ using namespace cv::dl;
 extern "C" int cv_decoder_input_supported(int n, int d, int features) {
   const int K = 2 * d;
   const int KR = K <= 16 ? 16 : K <= 32 ? 32 : K <= 64 ? 64 : 128;
-  return (n >= 1 && d >= 1 && K <= 128 && (long)((n + 15) & ~15) * KR <= ZMAX && features % DF == 0) ? 1 : 0;
+  // (d even: a latent pair never straddles the c / s halves, and the heads' pairs are 8-byte aligned)
+  return (n >= 1 && d >= 2 && d % 2 == 0 && K <= 128 && (long)((n + 15) & ~15) * KR <= ZMAX && features % DF == 0)
+             ? 1 : 0;
 }
 
 extern "C" int cv_decoder_input_forward(const cv_linear* g, const float* heads, const float* eps, uint64_t seed,
@@ -530,7 +539,7 @@ extern "C" int cv_decoder_input_forward(const cv_linear* g, const float* heads, 
   CV_REQUIRE(g->in_features % 2 == 0 && g->out_features == bn->C, "decoder_input_forward: bad shapes");
   const int d = g->in_features / 2, F = g->out_features;
   CV_REQUIRE(cv_decoder_input_supported(g->n, d, F), "decoder_input_forward: n=%d, K=%d, F=%d outside the fused "
-             "contract (n*K <= %d, K <= 128, F %% %d == 0)", g->n, 2 * d, F, ZMAX, DF);
+             "contract (d even, n*K <= %d, K <= 128, F %% %d == 0)", g->n, 2 * d, F, ZMAX, DF);
   CV_REQUIRE(!heads || eps || offset, "decoder_input_forward: need injected eps or a device offset counter");
   const int pix = g->out_pix > 0 ? g->out_pix : 1, ch = g->out_ch;
   CV_REQUIRE(pix <= 1 || pix * ch == F, "decoder_input_forward: out_pix*out_ch != out_features");

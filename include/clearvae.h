@@ -213,7 +213,7 @@ int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, 
  * mask, then the BN1d backward transform); gstat_out replica 0 receives the complete backward sums; gweight
  * [F][2d] += d(h)^T z.  dz = d(h) W is left to cv_linear_backward_data (no transform).  Replaces the two
  * launches of cv_declinear_backward_weight.  Contract: cv_decoder_input_supported(n, d, F) (n*2d <= 16384,
- * 2d <= 128, F % 16 == 0). */
+  * 2d <= 128, F % 16 == 0, d even). */
 int cv_decoder_input_supported(int n, int d, int features);
 int cv_decoder_input_forward(const cv_linear* g, const float* heads, const float* eps, uint64_t seed,
                              uint64_t* offset, float* z, const float* weight, const float* bias, const cv_bn* bn,
