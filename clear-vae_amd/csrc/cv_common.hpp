@@ -77,6 +77,8 @@ int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const floa
 int edge_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias, float* work,
                size_t work_bytes, hipStream_t st);
 size_t edge_wgrad_ws_bytes(const Geo& g, bool bias);
+int edge_bwd(const Geo& g, const cv_operand* gout, const float* wg, float* gin, const cv_epilogue* ep,
+             const cv_operand* x, float* gw, float* work, size_t work_bytes, hipStream_t st);
 
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {

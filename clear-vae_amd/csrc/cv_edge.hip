@@ -600,6 +600,217 @@ __global__ __launch_bounds__(ET) void edge_wgrad_kernel(const EArgs P) {
   }
 }
 
+// ---------------------------------------------------------------- ConvTranspose2d-to-image backward, both halves
+// The backward-data gather (big -> small, with the STAT_BWD epilogue of the small side's BatchNorm) and the
+// weight gradient (small x big) of the last ConvTranspose2d (vae.py:43 / :153) read the same band of the
+// image-side gradient (BN backward applied) and the same small-grid rows, whose BatchNorm (forward constants)
+// is both the epilogue's mask layer and the weight gradient's input transform.  One launch stages the big band
+// and the small rows once and runs both contractions; the staging, the MFMA order and the epilogue are those of
+// edge_gather_kernel and edge_wgrad_kernel, so the outputs are bit-identical to the two separate launches.
+// P: the gather's arguments (big = gout, out = gin, ep), Q: the weight gradient's (small = X, out = partials).
+template <int CB, int KK, int NT>
+__global__ __launch_bounds__(ET) void edge_bwd_kernel(const EArgs P, const EArgs Q) {
+  constexpr int NK = KK * KK * CB;
+  constexpr int KS = (NK + 3) / 4;
+  __shared__ BnFwdC kfs[CS];  // the small side's forward constants (weight-gradient transform, epilogue mask)
+  __shared__ BnBwdC kbs[CS];
+  __shared__ BnFwdC kfb[4];
+  __shared__ BnBwdC kbb[4];   // the big side's backward constants
+  __shared__ float red[ET / 64][2][CS];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Geo& g = P.g;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int kq = lane >> 4, nl = lane & 15;
+  const int n = blockIdx.y;
+  const int r0 = blockIdx.x * P.rows;
+  const int R = min(P.rows, g.hs - r0);
+  const int NC = (g.ws - 1) * g.s + KK;
+  const int NR = (R - 1) * g.s + KK;
+  // gather B fragments (packed gather weights [tap][cb][cs]) and tap-channel offsets
+  float bw[KS][2];
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    const int k = 4 * st + kq;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bw[st][j] = (k < NK) ? P.w[k * CS + 16 * j + nl] : 0.f;
+  }
+  int koff[KS];
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    const int k = 4 * st + kq;
+    const int tap = k / CB, c = k - tap * CB, kh = tap / KK, kw = tap - kh * KK;
+    koff[st] = (k < NK) ? (kh * NC + kw) * CB + c : 0;
+  }
+  // weight-gradient columns: offset in a receptive field, or -1 (bias: ones), -2 (padding: zeros)
+  const int ncol = Q.ncol;
+  int coff[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = 16 * j + nl;
+    if (col < NK) {
+      const int tap = col / CB, c = col - tap * CB, kh = tap / KK, kw = tap - kh * KK;
+      coff[j] = (kh * NC + kw) * CB + c;
+    } else {
+      coff[j] = (col < ncol) ? -1 : -2;
+    }
+  }
+  double* scratch = reinterpret_cast<double*>(lds);  // (fold scratch: the staging area, unused yet)
+  xf_consts(Q.small, kfs, kbs, scratch);
+  xf_consts(P.big, kfb, kbb, scratch);
+  __syncthreads();
+  float* sA = lds;                          // [R*ws][WP] small rows, transformed
+  float* sB = lds + (size_t)P.rows * g.ws * WP;  // [NR][NC][CB] big band, transformed
+  stage_small<WP>(g, Q.small, n, r0 * g.ws, R * g.ws, kfs, kbs, sA);
+  stage_big<CB>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kfb, kbb, sB);
+  __syncthreads();
+  const int npx = R * g.ws;
+  // ---- gather: out[px][32] = sum_k big[gather(px, k)] W[k][32]  (edge_gather_kernel's contraction)
+  int abase[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int px = 64 * w + 16 * i + nl;
+    const int rl = px / g.ws, xs = px - rl * g.ws;
+    abase[i] = (px < npx) ? ((rl * g.s) * NC + xs * g.s) * CB : 0;
+  }
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (64 * w < npx) {
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      float a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = sB[abase[i] + koff[st]];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bw[st][j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // ---- weight gradient: dW[o][col] = sum_px small[px][o] big[gather(px, col)]  (edge_wgrad_kernel's)
+  f32x4 wacc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) wacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    const FDiv fws = FDiv::make(g.ws);
+    for (int p0 = 4 * w; p0 < npx; p0 += 16) {
+      const int px = p0 + kq;
+      const bool ok = px < npx;
+      const int rl = fws.div(px), xs = px - rl * g.ws;
+      const int bb = ((rl * g.s) * NC + xs * g.s) * CB;
+      float a[2], b[NT];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = ok ? sA[px * WP + 16 * i + nl] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = coff[j] >= 0 ? (ok ? sB[bb + coff[j]] : 0.f) : (coff[j] == -1 && ok ? 1.f : 0.f);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) wacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], wacc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // (every wave is done with the staged operands)
+  // ---- gather epilogue through an LDS tile (edge_gather_kernel's)
+  float* sT = lds;
+  if (64 * w < npx) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = 64 * w + 16 * i + 4 * kq + r;
+        if (px >= npx) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sT[px * GP + 16 * j + nl] = acc[i][j][r];
+      }
+  }
+  __syncthreads();
+  const int mode = P.ep.stat_mode;
+  const int c0 = 4 * (t & 7);
+  BnFwdC kc[4];
+  if (mode == CV_STAT_BWD) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kc[k] = kfs[c0 + k];
+  }
+  f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+  const size_t pimg = ((size_t)n * g.hs + r0) * g.ws;
+  const int nq = npx * (CS / 4);
+  constexpr int UQ = 4;
+  for (int q0 = t; q0 < nq; q0 += ET * UQ) {
+    f32x4 y4[UQ];
+    if (mode == CV_STAT_BWD) {
+#pragma unroll
+      for (int u = 0; u < UQ; ++u) {
+        const int q = q0 + u * ET;
+        y4[u] = q < nq ? *reinterpret_cast<const f32x4*>(P.ep.ey + (pimg + (q >> 3)) * CS + c0) : s1;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int q = q0 + u * ET;
+      if (q >= nq) continue;
+      const int px = q >> 3;
+      f32x4 v = lds4(sT + px * GP + c0);
+      if (mode == CV_STAT_BWD) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (P.ep.erelu && bn_out(y4[u][k], kc[k]) <= 0.f) v[k] = 0.f;
+          s1[k] += v[k];
+          s2[k] += v[k] * ((y4[u][k] - kc[k].mu) * kc[k].istd);
+        }
+      }
+      *reinterpret_cast<f32x4*>(P.out + (pimg + px) * CS + c0) = v;
+    }
+  }
+  if (mode == CV_STAT_BWD) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int m = 8; m < 64; m <<= 1) {
+        s1[k] += __shfl_xor(s1[k], m, 64);
+        s2[k] += __shfl_xor(s2[k], m, 64);
+      }
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        red[w][0][c0 + k] = s1[k];
+        red[w][1][c0 + k] = s2[k];
+      }
+    }
+  }
+  __syncthreads();  // (the tile reads are complete: the fold area below reuses it; red is published)
+  if (mode == CV_STAT_BWD && t < 2 * CS) {
+    const int q = t / CS, col = t - q * CS;
+    double v = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < ET / 64; ++ww) v += (double)red[ww][q][col];
+    const int repl = (blockIdx.y * gridDim.x + blockIdx.x) % CV_STAT_REPL(CS);
+    atomic_add_f64(P.ep.stat_out + (size_t)repl * 2 * CS + q * CS + col, v);
+  }
+  // ---- weight-gradient partials: the waves' tiles folded in wave order (edge_wgrad_kernel's)
+  float* wred = lds;
+  const int NP = 16 * NT;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wred[((size_t)w * CS + 16 * i + 4 * kq + r) * NP + 16 * j + nl] = wacc[i][j][r];
+  __syncthreads();
+  float* part = Q.out + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * CS * ncol;
+  for (int e = t; e < CS * ncol; e += ET) {
+    const int o = e / ncol, col = e - o * ncol;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < ET / 64; ++ww) v += wred[((size_t)ww * CS + o) * NP + col];
+    part[e] = v;
+  }
+}
+
 // ---------------------------------------------------------------- host side
 static bool ep_ok(const cv_epilogue* ep, int C) {
   if (!ep || ep->stat_mode == CV_STAT_NONE) return true;
@@ -776,6 +987,62 @@ int edge_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, flo
   else CV_EDGE_PICK(edge_wgrad_kernel, , 4);
   if (launch(kern, dim3(nblk), lds, a, st, "edge_wgrad")) return 1;
   return wgrad_reduce_launch(work, nblk, CS, nk, a.ncol, g.cb, g.kh * g.kw, gw, gbias, st);
+}
+
+// Both halves of the ConvTranspose2d-to-image backward in one launch (edge_bwd_kernel), when the geometry is
+// the edge kernels' and the epilogue's BatchNorm is the weight gradient's input transform; -1 otherwise (the
+// caller runs edge_gather / edge_wgrad or the generic kernels)
+int edge_bwd(const Geo& g, const cv_operand* gout, const float* wg, float* gin, const cv_epilogue* ep,
+             const cv_operand* x, float* gw, float* work, size_t work_bytes, hipStream_t st) {
+  if (!geo_ok(g) || !work || !ep || ep->stat_mode != CV_STAT_BWD || !ep_ok(ep, CS)) return -1;
+  if (gout->xf != CV_XF_BNBWD || gout->nchw || gout->bn.C != g.cb || !gout->y) return -1;
+  if (x->xf != CV_XF_BNRELU || x->nchw || x->bn.C != CS) return -1;
+  const cv_bn &eb = ep->ebn, &xb = x->bn;  // the same layer on both sides
+  if (eb.stat != xb.stat || eb.cfwd != xb.cfwd || eb.ticket != xb.ticket || eb.gamma != xb.gamma || !eb.train ||
+      !xb.train)
+    return -1;
+  EArgs a, b;
+  memset(&a, 0, sizeof(a));
+  a.g = g;
+  a.big = *gout;
+  a.w = wg;
+  a.out = gin;
+  a.ep = *ep;
+  a.rows = edge_rows(g);
+  b = a;
+  b.small = *x;
+  const int nk = g.kh * g.kw * g.cb;
+  b.ncol = nk;
+  const int nblk = edge_wgrad_blocks(g);
+  if (work_bytes < (size_t)nblk * CS * b.ncol * sizeof(float)) return -1;
+  b.out = work;
+  const int kk = g.kh, cb = g.cb;
+  const int NR = (a.rows - 1) * g.s + kk, NC = (g.ws - 1) * g.s + kk;
+  const int NT = (b.ncol + 15) / 16;
+  size_t lds = ((size_t)a.rows * g.ws * WP + (size_t)NR * NC * cb) * sizeof(float);
+  const size_t tile = (size_t)a.rows * g.ws * GP * sizeof(float);
+  const size_t lred = (size_t)(ET / 64) * CS * 16 * NT * sizeof(float);
+  if (tile > lds) lds = tile;
+  if (lred > lds) lds = lred;
+  if (lds < 4 * ET * sizeof(double)) lds = 4 * ET * sizeof(double);
+  if (lds > 96 * 1024 || b.ncol > 64) return -1;
+  const void* kern = nullptr;
+  if (NT == 1) CV_EDGE_PICK(edge_bwd_kernel, , 1);
+  else if (NT == 2) CV_EDGE_PICK(edge_bwd_kernel, , 2);
+  else if (NT == 3) CV_EDGE_PICK(edge_bwd_kernel, , 3);
+  else CV_EDGE_PICK(edge_bwd_kernel, , 4);
+  if (!kern) return -1;
+  if (set_lds(kern, lds)) {
+    set_error("edge_bwd: LDS carve-out of %zu bytes refused", lds);
+    return 1;
+  }
+  void* params[] = {&a, &b};
+  if (hipLaunchKernel(kern, dim3(cdiv(g.hs, a.rows), g.n), dim3(ET), params, lds, st) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("edge_bwd: launch failed");
+    return 2;
+  }
+  return wgrad_reduce_launch(work, nblk, CS, nk, b.ncol, g.cb, g.kh * g.kw, gw, nullptr, st);
 }
 
 }  // namespace cv

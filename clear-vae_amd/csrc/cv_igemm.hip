@@ -1430,6 +1430,24 @@ extern "C" int cv_conv_backward_weight_deferred(const cv_conv* g, const cv_opera
   return r;
 }
 
+extern "C" int cv_conv_backward_deferred(const cv_conv* g, const cv_operand* gout, const float* wpacked, float* gin,
+                                         const cv_epilogue* ep, const cv_operand* in, float* gweight, float* gbias,
+                                         float* work, size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t stream) {
+  clear_error();
+  if (check_conv(g) || check_operand(gout, "conv_backward") || check_operand(in, "conv_backward")) return 1;
+  CV_REQUIRE(wpacked && gin && gweight && defer && work, "conv_backward: null weight / gin / gweight / defer / work");
+  if (g->transposed && !gbias && !g_force_generic) {  // the image-side ConvTranspose2d: one launch for both halves
+    memset(defer, 0, sizeof(*defer));
+    g_defer_sink = defer;
+    const int r = edge_bwd(geo_of(g), gout, wpacked, gin, ep, in, gweight, work, work_bytes, S(stream));
+    g_defer_sink = nullptr;
+    if (r >= 0) return r;
+  }
+  const int r = cv_conv_backward_data(g, gout, wpacked, gin, ep, stream);
+  if (r) return r;
+  return cv_conv_backward_weight_deferred(g, in, gout, gweight, gbias, work, work_bytes, defer, stream);
+}
+
 // ---------------------------------------------------------------- linear layers
 static int linear_launch(Args& a, int accumulate, hipStream_t st) {
   int BM_, BN_;

@@ -608,13 +608,31 @@ class Workspace:
             else:
                 P.add_side("cv_linear_backward_weight", geom, a, b, gw, gb, 0, self.wg_work, self.wg_bytes)
             return
+        buf = self._defer_buf(kind, geom, key)
+        name = "cv_conv_backward_weight_deferred" if kind == "conv" else "cv_linear_backward_weight_deferred"
+        P.add(name, geom, a, b, gw, gb, buf, buf.numel() * 4, defer.next())
+
+    def _defer_buf(self, kind: str, geom, key):
+        L = _lib.lib()
         nb = int((L.cv_conv_wgrad_workspace_bytes if kind == "conv" else L.cv_linear_wgrad_workspace_bytes)(
             ctypes.byref(geom), 0))
         buf = self._defer_work.get(key)
         if buf is None or buf.numel() * 4 < nb:
             buf = self._defer_work[key] = torch.empty(max(nb, 16) // 4 + 4, dtype=torch.float32, device=self.device)
-        name = "cv_conv_backward_weight_deferred" if kind == "conv" else "cv_linear_backward_weight_deferred"
-        P.add(name, geom, a, b, gw, gb, buf, buf.numel() * 4, defer.next())
+        return buf
+
+    # cv_conv_backward_deferred: data and deferred weight gradient of a layer in one call (one launch for the
+    # image-side ConvTranspose2d; CVHIP_FUSED_EDGE_BWD=0: the two calls)
+    FUSED_EDGE_BWD = os.environ.get("CVHIP_FUSED_EDGE_BWD", "1") != "0"
+
+    def _conv_backward(self, P: "Program", geom, gout, wpacked, gin, ep, xin, gw, key, defer):
+        if defer is None or not self.FUSED_EDGE_BWD:
+            P.add("cv_conv_backward_data", geom, gout, wpacked, gin, ep)
+            self._wgrad_call(P, "conv", geom, xin, gout, gw, None, key, defer)
+            return
+        buf = self._defer_buf("conv", geom, key)
+        P.add("cv_conv_backward_deferred", geom, gout, wpacked, gin, ep, xin, gw, None, buf, buf.numel() * 4,
+              defer.next())
 
     def _views(self, which) -> list:
         """BN layers by name ('all', 'enc', 'dec') or an explicit list of BNViews (a gradient bucket's)."""
@@ -750,8 +768,10 @@ class Workspace:
             gout = operand(self.g_dec[li], XF_BNBWD, self.bn_dec[li].cv(True), y=self.y_dec[li])
             if li > 0:
                 ep = ep_bwd(self.bn_dec[li - 1], self.y_dec[li - 1], sp.dec[li - 1].relu)
-                P.add("cv_conv_backward_data", g, gout, c.wbwd, self.g_dec[li - 1], ep)
                 xin = operand(self.y_dec[li - 1], XF_BNRELU, self.bn_dec[li - 1].cv(True))
+                self._conv_backward(P, g, gout, c.wbwd, self.g_dec[li - 1], ep, xin, param_grad(c.mod.weight),
+                                    ("dec", li), defer)
+                continue
             else:
                 P.add("cv_conv_backward_data", g, gout, c.wbwd, self.gah, ep_none())
                 xin = operand(self.ah)

@@ -164,6 +164,14 @@ int cv_conv_backward_weight_deferred(const cv_conv* g, const cv_operand* in, con
                                      float* gweight, float* gbias, float* work, size_t work_bytes,
                                      cv_wgrad_defer* defer, cv_stream_t stream);
 
+/* Both halves of a conv / convT backward (aten::convolution_backward, trainer.py:482): dx as
+ * cv_conv_backward_data and the deferred weight gradient as cv_conv_backward_weight_deferred, in one launch for
+ * the image-side ConvTranspose2d (vae.py:43 / :153: the edge kernels' geometry, ep's BatchNorm = in's
+ * transform), otherwise the two launches in that order. */
+int cv_conv_backward_deferred(const cv_conv* g, const cv_operand* gout, const float* wpacked, float* gin,
+                              const cv_epilogue* ep, const cv_operand* in, float* gweight, float* gbias, float* work,
+                              size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t stream);
+
 /* ---- fully connected layers (nn.Linear heads vae.py:27-30; decoder Linear vae.py:33) ----
  * A linear layer whose input (or output) is the NCHW-flattened view of an NHWC activation with
  * `*_pix` pixels and `*_ch` channels (nn.Flatten vae.py:25 / nn.Unflatten vae.py:36).              */
