@@ -499,6 +499,155 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
   if (A.gstat_out) bn_finalize<NTD>(A.bn, A.gstat_out, true, reinterpret_cast<double*>(smem), &flag);
 }
 
+// ---------------------------------------------------------------- encoder heads forward (+ reparameterisation)
+// heads = ReLU(BN(y)) W^T + b over the Flatten of the last conv block (vae.py:25-30), and, optionally, the
+// reparameterisation z = mu + eps * exp(logvar / 2) of the workgroup's rows (vae.py:56-60, the arithmetic and
+// the Philox pair indexing of reparam_kernel).  A workgroup owns 16 rows and one column group: the 16-column tile
+// of some mu block and the tile of its logvar partner (d % 16 == 0), or, for d = 8, the one tile holding both
+// (mu | logvar of 8 latents), so each latent's mu and logvar meet in one workgroup.  Its 8 waves split K (the
+// F flattened features, staged straight from global in 16-byte rows with the BN + ReLU transform of the
+// storage channel) and fold their partial tiles in LDS in wave order.  B comes from the heads weight packed
+// [F (storage order)][4d] by the step's pack launch (cv_conv_pack with cs = 4d, cb = C, kh x kw = the pixels).
+struct HeadsFwdArgs {
+  const float* y;       // [n][F] storage order (pixel-major, C channels)
+  cv_bn bn;             // the last conv block's BatchNorm2d (train: finalised cfwd or replica sums)
+  const float* wp;      // [F][J] packed heads weight (row = storage feature)
+  const float* bias;    // [J]
+  float* heads;         // [n][J]
+  const float* eps;     // reparameterisation: injected [n][2d] or Philox(seed, offset[0]); z == nullptr: none
+  uint64_t seed;
+  uint64_t* offset;
+  float* z;             // [n][2d]
+  int n, d, J, F, ch, ngrp, jt;  // jt: 16-column tiles per group (1: d = 8, 2: d % 16 == 0)
+};
+
+constexpr int HF_NT = 1024;
+template <int JT>
+__global__ __launch_bounds__(HF_NT) void heads_fwd_kernel(const HeadsFwdArgs A) {
+  constexpr int NWV = HF_NT / 64;
+  __shared__ float cst[3][512];        // BN sc, mu, beta per channel (C <= 512)
+  __shared__ float red[NWV][JT][16][17];
+  __shared__ float hs[16][2 * 16 + 1];  // the group's summed tiles (+ bias)
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
+  const int n = A.n, F = A.F, C = A.ch, d = A.d, J = A.J;
+  const int rb = blockIdx.x / A.ngrp, gi = blockIdx.x - rb * A.ngrp;
+  const int row0 = 16 * rb;
+  // the group's columns: tile 0 (and tile 1, the logvar partner)
+  int c0[2];
+  if (JT == 1) {
+    c0[0] = 16 * gi;  // d = 8: [mu | logvar] of half gi
+    c0[1] = c0[0];
+  } else {
+    const int per = d / 16, h = gi / per, m = gi - h * per;
+    c0[0] = h * 2 * d + 16 * m;
+    c0[1] = c0[0] + d;
+  }
+  const uint64_t off = (A.z && A.offset) ? A.offset[0] : 0;
+  // BN constants of every channel (finalised by the producing conv, else folded)
+  {
+    const cv_bn& b = A.bn;
+    const bool fin = b.train && b.cfwd && b.ticket && b.ticket[0] != 0u;
+    for (int c = t; c < C; c += HF_NT) {
+      BnFwdC k;
+      if (fin) k = BnFwdC{b.cfwd[c], b.cfwd[C + c], b.cfwd[2 * C + c], b.cfwd[3 * C + c]};
+      else k = bn_fwd_const(b, c);
+      cst[0][c] = k.sc;
+      cst[1][c] = k.mu;
+      cst[2][c] = k.be;
+    }
+  }
+  __syncthreads();
+  // wave w contracts K slice [w F / NWV, (w + 1) F / NWV) in 16-wide chunks; lane (lr, lq) feeds row lr and
+  // k = 16 c + 4 lq + s
+  const int kper = F / NWV;  // (host: F % (16 * NWV) == 0)
+  const int kb = w * kper;
+  const int row = row0 + lr;
+  const float* yr = A.y + (size_t)(row < n ? row : 0) * F;
+  f32x4 acc[JT];
+#pragma unroll
+  for (int j = 0; j < JT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int CB = 4;  // chunks per load batch
+  for (int k0 = kb; k0 < kb + kper; k0 += 16 * CB) {
+    f32x4 av[CB];
+    float bv[CB][JT][4];
+#pragma unroll
+    for (int q = 0; q < CB; ++q) {
+      const int k = k0 + 16 * q + 4 * lq;
+      av[q] = *reinterpret_cast<const f32x4*>(yr + k);
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bv[q][j][s] = A.wp[(size_t)(k + s) * J + c0[j] + lr];
+    }
+#pragma unroll
+    for (int q = 0; q < CB; ++q) {
+      const int k = k0 + 16 * q + 4 * lq;
+      const int c = k % C;  // 4 consecutive channels of one pixel (C % 4 == 0)
+      f32x4 a = av[q];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        a[s] = fmaxf(fmaf(a[s] - cst[1][c + s], cst[0][c + s], cst[2][c + s]), 0.f);
+        if (row >= n) a[s] = 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bv[q][j][s], acc[j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < JT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][j][4 * lq + r][lr] = acc[j][r];
+  __syncthreads();
+  for (int e = t; e < JT * 256; e += HF_NT) {  // fold the waves in order, add the bias, store
+    const int j = e / 256, rr = (e / 16) % 16, cc = e % 16;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NWV; ++ww) v += red[ww][j][rr][cc];
+    const int col = c0[j] + cc;
+    v += A.bias ? A.bias[col] : 0.f;
+    hs[rr][16 * j + cc] = v;
+    if (row0 + rr < n) A.heads[(size_t)(row0 + rr) * J + col] = v;
+  }
+  if (!A.z) return;
+  __syncthreads();
+  // reparameterisation of the group's latents (pair p = elements 2p, 2p + 1 of z [n][2d], as reparam_kernel)
+  const int half = (JT == 1) ? gi : (c0[0] >= 2 * d ? 1 : 0);  // 0: z_c, 1: z_s
+  const int lat0 = (JT == 1) ? 0 : c0[0] - half * 2 * d;      // first latent of the group within its half
+  const int nl = (JT == 1) ? d : 16;                           // latents of the group
+  for (int e = 2 * t; e < 16 * nl; e += 2 * HF_NT) {
+    const int rr = e / nl, m = e - rr * nl;  // (nl even: a pair stays in one row)
+    const int grow = row0 + rr;
+    if (grow >= n) continue;
+    const int zj = half * d + lat0 + m;  // z column of the first element
+    const long ez = (long)grow * 2 * d + zj;
+    float e2[2];
+    if (A.eps) {
+      e2[0] = A.eps[ez];
+      e2[1] = A.eps[ez + 1];
+    } else {
+      normal2(A.seed, off, (uint64_t)(ez >> 1), e2[0], e2[1]);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float mu = hs[rr][m + q];
+      const float lv = hs[rr][(JT == 1 ? d : 16) + m + q];
+      A.z[ez + q] = mu + e2[q] * expf(0.5f * lv);
+    }
+  }
+  if (A.offset) {  // the last workgroup to finish advances the noise counter
+    __syncthreads();
+    if (t == 0) {
+      const unsigned long long prev = atomicAdd((unsigned long long*)(A.offset + 1), 1ull);
+      if (prev == (unsigned long long)(gridDim.x - 1)) {
+        A.offset[0] = off + 1;
+        A.offset[1] = 0;
+      }
+    }
+  }
+}
+
 template <class Fn>
 static int pick_kr(int K, Fn fn) {
   if (K <= 16) return fn(std::integral_constant<int, 16>());
@@ -661,4 +810,45 @@ extern "C" int cv_heads_backward(const cv_linear* g, const float* dheads, const 
   if (a.J <= 32) return go(std::integral_constant<int, 32>());
   if (a.J <= 64) return go(std::integral_constant<int, 64>());
   return go(std::integral_constant<int, 128>());
+}
+
+extern "C" int cv_heads_forward_supported(int n, int in_features, int in_ch, int d) {
+  return (n >= 1 && in_ch % 4 == 0 && in_ch <= 512 && in_features % (16 * (HF_NT / 64)) == 0 &&
+          (d == 8 || (d % 16 == 0 && d <= 64))) ? 1 : 0;
+}
+
+extern "C" int cv_heads_forward(const cv_linear* g, const float* y, const cv_bn* bn, const float* wpacked,
+                                const float* bias, float* heads, const float* eps, uint64_t seed, uint64_t* offset,
+                                float* z, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(g && y && bn && wpacked && heads, "heads_forward: null args");
+  const int pix = g->in_pix > 0 ? g->in_pix : 1, ch = pix > 1 ? g->in_ch : g->in_features;
+  CV_REQUIRE(pix * ch == g->in_features && bn->C == ch && g->out_features % 4 == 0,
+             "heads_forward: in_pix*in_ch != in_features, BN C != in_ch or 4d not a multiple of 4");
+  const int d = g->out_features / 4;
+  CV_REQUIRE(cv_heads_forward_supported(g->n, g->in_features, ch, d), "heads_forward: n=%d, F=%d, C=%d, d=%d outside "
+             "the fused contract", g->n, g->in_features, ch, d);
+  CV_REQUIRE(!z || eps || offset, "heads_forward: the reparameterisation needs injected eps or an offset counter");
+  HeadsFwdArgs a;
+  a.y = y;
+  a.bn = *bn;
+  a.wp = wpacked;
+  a.bias = bias;
+  a.heads = heads;
+  a.eps = eps;
+  a.seed = seed;
+  a.offset = z ? offset : nullptr;
+  a.z = z;
+  a.n = g->n;
+  a.d = d;
+  a.J = g->out_features;
+  a.F = g->in_features;
+  a.ch = ch;
+  a.jt = d == 8 ? 1 : 2;
+  a.ngrp = d == 8 ? 2 : 2 * (d / 16);
+  const dim3 grid(cdiv(g->n, 16) * a.ngrp);
+  if (a.jt == 1) hipLaunchKernelGGL(heads_fwd_kernel<1>, grid, dim3(HF_NT), 0, S(stream), a);
+  else hipLaunchKernelGGL(heads_fwd_kernel<2>, grid, dim3(HF_NT), 0, S(stream), a);
+  CV_LAUNCH_CHECK("heads_forward");
+  return 0;
 }

@@ -211,6 +211,12 @@ _SIGS = {
         c_int,
         [_P(cv_linear), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "cv_heads_forward_supported": (c_int, [c_int, c_int, c_int, c_int]),
+    "cv_heads_forward": (
+        c_int,
+        [_P(cv_linear), c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+         c_void_p],
+    ),
     "cv_heads_backward_supported": (c_int, [c_int, c_int, c_int, c_int]),
     "cv_heads_backward": (
         c_int,

@@ -312,7 +312,8 @@ class ClearStep:
             bufs = [(ws.stats, ws.stats.numel() * 8), (A.grad, A.numel * 4), (ws.heads, ws.heads.numel() * 4),
                     (ws.dz, ws.dz.numel() * 4)]
             pack_program(sp, f, "all", zero=bufs)
-            ws.encoder_program(f, X, True, zero_heads=False)
+            rp = None if grouped else (eps_buf[0] if inject else None, self.seed, self.offset)
+            drew = ws.encoder_program(f, X, True, zero_heads=False, reparam=rp)
             if grouped:
                 hb = ws.heads.data_ptr()
                 f.add("cv_group_forward", self.group_mode, hb, hb + 4 * d, 4 * d, lab, n, d, gwork, gscale_rec,
@@ -321,8 +322,7 @@ class ClearStep:
                 ws.decoder_program(f, ws.z, True, "loss", X, rec_scale=gscale_rec)
                 f.keep += [gwork, gscale_rec]
             else:
-                ws.decoder_program(f, ws.z, True, "loss", X,
-                                   reparam=(eps_buf[0] if inject else None, self.seed, self.offset))
+                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp)
             # (the running statistics are folded at the end of the backward by cv_step_reduce)
             return f
 
@@ -427,13 +427,15 @@ class ClearStep:
             # (its statistics follow z) and the running-statistics update of every layer (the encoder's five
             # momentum updates with its one set of batch statistics, as in five forwards)
             def learn_forward(prog, j, inject):
+                rp = (eps_buf[1 + j] if inject else None, self.seed, self.offset)
                 if j == 0:
                     prog.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-                    ws.encoder_program(prog, X, True)
+                    if ws.encoder_program(prog, X, True, reparam=rp):
+                        return None  # (z drawn by the heads launch)
                 else:
                     prog.add("cv_zero_many", ptr_array([ws.dec_stats.data_ptr(), ws.dec_tickets.data_ptr()]),
                              (ctypes.c_size_t * 2)(ws.dec_stats.numel() * 8, ws.dec_tickets.numel() * 8), 2)
-                return (eps_buf[1 + j] if inject else None, self.seed, self.offset)
+                return rp
 
             def make_learn(inject: bool):
                 lp = Program()
@@ -479,9 +481,9 @@ class ClearStep:
                 gp = Program()
                 pack_program(sp, gp, "all")  # the VAE Adam step just moved the weights
                 gp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
-                ws.encoder_program(gp, X, True)
-                ws.decoder_program(gp, ws.z, True, "none",
-                                   reparam=(eps_buf[1] if inject else None, self.seed, self.offset))
+                rp = (eps_buf[1] if inject else None, self.seed, self.offset)
+                drew = ws.encoder_program(gp, X, True, reparam=rp)
+                ws.decoder_program(gp, ws.z, True, "none", reparam=None if drew else rp)
                 ws.running_program(gp, "all")
                 gp.add("cv_tc_learning_step", disc, ws.z, n, tc_work, self.learn, G)
                 ap = Program()

@@ -287,6 +287,12 @@ def attach_packed(spec: VaeSpec, device):
                 cv_conv_pack(w.data_ptr(), gat.data_ptr(), sca.data_ptr(), w.shape[0], w.shape[1], w.shape[2],
                              w.shape[3]))
     spec.packed = buf
+    # the four heads as one [4d][F] weight, packed [F (storage order)][4d] for cv_heads_forward: the conv pack's
+    # gather order with cs = 4d, cb = C and the pixels as taps
+    C, Hh, Wh = spec.feat
+    hw = spec.heads[0].weight
+    spec.heads_wp = torch.empty(4 * spec.d * spec.F, dtype=torch.float32, device=device)
+    spec.pack_items["enc"].append(cv_conv_pack(hw.data_ptr(), spec.heads_wp.data_ptr(), None, 4 * spec.d, C, Hh, Wh))
 
 
 def pack_program(spec: VaeSpec, P: "Program", which: str = "all", zero=None):
@@ -666,13 +672,25 @@ class Workspace:
         P = Program()
         if train:
             P.add("cv_zero", self.stats, self.stats.numel() * 8)
-        self.encoder_program(P, x, train)
-        self.decoder_program(P, self.z, train, output, x, rec_scale, reparam=(eps, seed, offset))
+        drew = self.encoder_program(P, x, train, reparam=(eps, seed, offset))
+        self.decoder_program(P, self.z, train, output, x, rec_scale, reparam=None if drew else (eps, seed, offset))
         if train:
             self.running_program(P, "all")
         return P
 
-    def encoder_program(self, P: Program, x, train: bool, zero_heads: bool = True):
+    # cv_heads_forward (cv_declinear.hip): the heads and the reparameterisation of their rows in one launch
+    # (CVHIP_FUSED_HEADS_FWD=0: the DENSE split-K GEMM, the reparameterisation inside the decoder-input launch)
+    FUSED_HEADS_FWD = os.environ.get("CVHIP_FUSED_HEADS_FWD", "1") != "0"
+
+    def fused_heads_forward(self) -> bool:
+        sp = self.spec
+        C, Hh, Wh = sp.feat
+        return (self.FUSED_HEADS_FWD and getattr(sp, "heads_wp", None) is not None
+                and bool(_lib.lib().cv_heads_forward_supported(self.n, sp.F, C, sp.d)))
+
+    def encoder_program(self, P: Program, x, train: bool, zero_heads: bool = True, reparam=None) -> bool:
+        """Encoder + heads.  reparam = (eps, seed, offset): also draw z in the heads launch when the fused heads
+        kernel serves this shape; returns True if it did (the caller then decodes z as given)."""
         sp, n = self.spec, self.n
         cur = None
         for li, c in enumerate(sp.enc):
@@ -684,13 +702,21 @@ class Workspace:
             ep = ep_fwd(self.bn_enc[li]) if train else ep_none()
             P.add("cv_conv_forward", g, op, c.wfwd, c.mod.bias, self.y_enc[li], ep)
             cur = self.y_enc[li]
-        # heads (Linear on the NCHW-flattened activation), split-K into a zeroed buffer
+        # heads (Linear on the NCHW-flattened activation)
         C, Hh, Wh = sp.feat
         lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
+        if self.fused_heads_forward():
+            eps, seed, offset = reparam if reparam is not None else (None, 0, None)
+            P.add("cv_heads_forward", lin, cur, self.bn_enc[-1].cv(train), sp.heads_wp, sp.heads[0].bias.data_ptr(),
+                  self.heads, eps.data_ptr() if eps is not None else None, ctypes.c_uint64(seed),
+                  offset.data_ptr() if offset is not None else None, self.z if reparam is not None else None)
+            return reparam is not None
+        # split-K into a zeroed buffer
         if zero_heads:  # (else the caller zeroed it earlier in the same program)
             P.add("cv_zero", self.heads, self.heads.numel() * 4)
         P.add("cv_linear_forward", lin, operand(cur, XF_BNRELU, self.bn_enc[-1].cv(train)),
               sp.heads[0].weight.data_ptr(), sp.heads[0].bias.data_ptr(), self.heads, 1, ep_none())
+        return False
 
     def reparam_program(self, P: Program, eps=None, seed: int = 0, offset=None):
         P.add("cv_reparam_forward", self.heads, self.n, self.spec.d, eps.data_ptr() if eps is not None else None,

@@ -229,6 +229,16 @@ int cv_decoder_input_forward(const cv_linear* g, const float* heads, const float
 int cv_decoder_input_backward(const cv_linear* g, float* ga, const float* h, const cv_bn* bn, double* gstat_out,
                               const float* z, float* gweight, cv_stream_t stream);
 
+/* Encoder heads forward in one launch (the four nn.Linear heads vae.py:27-30 over the Flatten of the last conv
+ * block vae.py:25, its BatchNorm2d + ReLU applied to y on load): heads [n][4d] = ReLU(BN(y)) W^T + bias with W
+ * packed [in_features (storage order)][4d] (cv_conv_pack of the [4d][C][Hh][Wh] view, `gather` order), and, when
+ * z != NULL, the reparameterisation of its rows exactly as cv_reparam_forward (vae.py:56-60).  Replaces
+ * cv_linear_forward of the heads (+ cv_reparam_forward).  Contract: cv_heads_forward_supported(n,
+ * in_features, in_ch, d) (d = 8 or a multiple of 16 up to 64, in_ch % 4 == 0, in_ch <= 512). */
+int cv_heads_forward_supported(int n, int in_features, int in_ch, int d);
+int cv_heads_forward(const cv_linear* g, const float* y, const cv_bn* bn, const float* wpacked, const float* bias,
+                     float* heads, const float* eps, uint64_t seed, uint64_t* offset, float* z, cv_stream_t stream);
+
 /* Encoder heads backward in one launch (the four nn.Linear heads vae.py:27-30 as one [4d][F] weight over the
  * Flatten of the last conv block, vae.py:25; trainer.py:482): gin [n][F] (storage order in_pix/in_ch) =
  * (dheads W) * [BN(y) > 0] with that BatchNorm2d's backward sums added to gstat_out (fp64 replicas; the layer's

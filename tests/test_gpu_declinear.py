@@ -214,3 +214,65 @@ def test_heads_backward(n, C, pix, J, finalise):
         assert int(ticket[1]) == (nblk + gsz - 1) // gsz
     else:
         assert float(cbwd.abs().max()) == 0.0
+
+
+HEADS_FWD = [  # n, C, (Hh, Wh), d
+    (512, 128, (4, 4), 8),
+    (256, 512, (2, 2), 32),
+    (37, 128, (4, 4), 8),
+]
+
+
+@pytest.mark.parametrize("n,C,hw,d", HEADS_FWD)
+@pytest.mark.parametrize("finalised", [False, True])
+def test_heads_forward_reparam(n, C, hw, d, finalised):
+    """cv_heads_forward (vae.py:25-30 heads on ReLU(BN(y)), then VAE.sample vae.py:56-60) against fp64, with the
+    weight packed by cv_pack_conv_weights; z bit-identical to cv_reparam_forward on the kernel's heads."""
+    from cvhip import _lib
+
+    dev = torch.device("cuda")
+    Hh, Wh = hw
+    pix, F, J = Hh * Wh, C * Hh * Wh, 4 * d
+    assert _lib.lib().cv_heads_forward_supported(n, F, C, d) == 1
+    g = np.random.default_rng(n + d + C)
+    y = torch.tensor(g.standard_normal((n, F)) + 0.2, dtype=torch.float32, device=dev)  # storage order
+    W = torch.tensor(g.uniform(-0.05, 0.05, (J, F)), dtype=torch.float32, device=dev)
+    b = torch.tensor(g.uniform(-0.1, 0.1, J), dtype=torch.float32, device=dev)
+    gamma = torch.tensor(g.uniform(0.5, 1.5, C), dtype=torch.float32, device=dev)
+    beta = torch.tensor(g.uniform(-0.3, 0.3, C), dtype=torch.float32, device=dev)
+    yc = y.double().view(n * pix, C)
+    mean, var = yc.mean(0), yc.var(0, unbiased=False)
+    istd = 1.0 / torch.sqrt(var + 1e-5)
+    R = _lib.stat_repl(C)
+    stat = torch.zeros(R, 2, C, dtype=torch.float64, device=dev)
+    stat[0, 0] = yc.sum(0)
+    stat[0, 1] = (yc * yc).sum(0)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    cfwd = torch.cat([(gamma.double() * istd), mean, beta.double(), istd]).float().to(dev)
+    ticket = torch.zeros(_lib.TICKET_WORDS, dtype=torch.int32, device=dev)
+    ticket[0] = 1
+    bn = _lib.cv_bn(gamma.data_ptr(), beta.data_ptr(), stat.data_ptr(), stat.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                    C, n * pix, 1, 1e-5, None if not finalised else None, None, None)
+    if finalised:
+        bn.cfwd = cfwd.data_ptr()
+        bn.ticket = ticket.data_ptr()
+    wp = torch.empty(F * J, device=dev)
+    item = (_lib.cv_conv_pack * 1)(_lib.cv_conv_pack(W.data_ptr(), wp.data_ptr(), None, J, C, Hh, Wh))
+    s = _lib.stream_handle()
+    _lib.call("cv_pack_conv_weights", item, 1, s)
+    lin = _lib.cv_linear(n, F, J, pix, C, 1, 0, 0)
+    heads = torch.empty(n, J, device=dev)
+    z = torch.empty(n, 2 * d, device=dev)
+    off = torch.tensor([3, 0], dtype=torch.int64, device=dev)
+    _lib.call("cv_heads_forward", ctypes.byref(lin), y.data_ptr(), ctypes.byref(bn), wp.data_ptr(), b.data_ptr(),
+              heads.data_ptr(), None, ctypes.c_uint64(99), off.data_ptr(), z.data_ptr(), s)
+    z_ref = torch.empty(n, 2 * d, device=dev)
+    off_ref = torch.tensor([3, 0], dtype=torch.int64, device=dev)
+    _lib.call("cv_reparam_forward", heads.data_ptr(), n, d, None, ctypes.c_uint64(99), off_ref.data_ptr(),
+              z_ref.data_ptr(), None, s)
+    torch.cuda.synchronize()
+    a = torch.relu(((yc - mean) * istd * gamma.double() + beta.double())).view(n, pix, C).permute(0, 2, 1)
+    ref = a.reshape(n, F) @ W.double().T + b.double()
+    assert _rel(heads, ref) < 1e-5
+    assert torch.equal(z, z_ref), "z differs from cv_reparam_forward on the same heads"
+    assert off.tolist() == [4, 0]
