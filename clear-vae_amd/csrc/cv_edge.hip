@@ -812,6 +812,19 @@ __global__ __launch_bounds__(ET) void edge_bwd_kernel(const EArgs P, const EArgs
 }
 
 // ---------------------------------------------------------------- host side
+// small-grid rows per band of the gather / weight-gradient / fused backward launches: one row per thread
+// (ET / ws), at most the image; CV_EDGE_ROWS=<rows> overrides (A/B knob)
+static int edge_rows(const Geo& g) {
+  static int ovr = -2;
+  if (ovr == -2) {
+    const char* e = getenv("CV_EDGE_ROWS");
+    ovr = e ? atoi(e) : -1;
+  }
+  int r = g.ws >= ET ? 1 : ET / g.ws;
+  if (ovr > 0) r = ovr;
+  return r > g.hs ? g.hs : r;
+}
+
 static bool ep_ok(const cv_epilogue* ep, int C) {
   if (!ep || ep->stat_mode == CV_STAT_NONE) return true;
   if (!ep->stat_out || ep->stat_div > 1) return false;
@@ -878,8 +891,7 @@ int edge_gather(const Geo& g, const cv_operand* in, const float* wg, const float
   a.out = out;
   if (ep) a.ep = *ep;
   else a.ep.stat_mode = CV_STAT_NONE;
-  a.rows = g.ws >= ET ? 1 : ET / g.ws;
-  if (a.rows > g.hs) a.rows = g.hs;
+  a.rows = edge_rows(g);
   const int kk = g.kh, cb = g.cb;
   size_t lds = (size_t)((a.rows - 1) * g.s + kk) * ((g.ws - 1) * g.s + kk) * cb * sizeof(float);
   const size_t tile = (size_t)a.rows * g.ws * GP * sizeof(float);  // the epilogue's output tile
@@ -940,10 +952,7 @@ int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const floa
   return launch(kern, dim3(cdiv(nby, rb), g.n), lds, a, st, "edge_scatter");
 }
 
-static int edge_rows(const Geo& g) {
-  const int r = g.ws >= ET ? 1 : ET / g.ws;
-  return r > g.hs ? g.hs : r;
-}
+
 
 // workgroups of the weight-gradient split, one per (image, band) (also sizes its workspace)
 static int edge_wgrad_blocks(const Geo& g) { return g.n * cdiv(g.hs, edge_rows(g)); }

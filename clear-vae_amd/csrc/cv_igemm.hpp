@@ -53,6 +53,12 @@ struct Args {
   // sums the slabs in slice order and runs the epilogue.  Null: no split.
   float* fix_part;
   unsigned* fix_cnt;
+  // XCD-grouped tile order (specialised core, GATHER / SCATTER without a K split; WGRAD: M-tile-fastest order):
+  // hardware workgroup id t runs on XCD t % 8, and every XCD gets a contiguous range of logical tiles enumerated
+  // minor-first over the tiles that read the same operand (SCATTER: the s^2 parity classes and N tiles of one
+  // small-grid tile; GATHER: the N tiles of one M tile; WGRAD: the M tiles of one (N tile, K split)), so each
+  // operand tile is fetched into one XCD's L2 once
+  int xcd;
   // fast divisors (filled by finalize_divs at launch)
   FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
 };
