@@ -309,8 +309,20 @@ void gemm_kernel2(const Args P) {
   };
   // the host clamps the grid to at most `tiles` workgroups; the guard keeps a workgroup without a tile
   // (a grid larger than the tile count) from decoding a bogus tile (a parity class bz >= tiles_z)
-  if (hw_id < nwg) tile_body(hw_id);
-  if (hw_id + (int)gridDim.x < nwg) tile_body(hw_id + (int)gridDim.x);
+  // (the tile body is inlined at exactly two call sites: more would grow the kernel past its register budget)
+  const int G = (int)gridDim.x;
+  int t1 = hw_id < nwg ? hw_id : -1, t2 = hw_id + G < nwg ? hw_id + G : -1;
+  if (OP == OP_SCATTER && P.bal_ncls) {
+    // K-balanced pairing: tiles sorted by their class's taps (heaviest class first); the workgroups with one
+    // tile take the heaviest, and the others pair the i-th heaviest remaining tile with the i-th lightest
+    const int S0 = nwg - G, single = G - S0, per = gx * gy;
+    const int p1 = hw_id >= S0 ? hw_id - S0 : single + hw_id, p2 = single + 2 * S0 - 1 - hw_id;
+    const int k1 = p1 / per, k2 = p2 / per;
+    t1 = p1 - k1 * per + per * P.cls_order[k1];
+    t2 = hw_id < S0 ? p2 - k2 * per + per * P.cls_order[k2] : -1;
+  }
+  if (t1 >= 0) tile_body(t1);
+  if (t2 >= 0) tile_body(t2);
   finalize(true);
 }
 
@@ -384,6 +396,13 @@ inline bool deep_enabled() {
 inline int env_flag(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? (atoi(e) != 0) : dflt;
+}
+// CV_BAL=1: the two-tile SCATTER launches pair their tiles K-balanced (Args::bal_ncls) instead of w and w + G
+// in class-major order; measured neutral (MNIST 0.5802 vs 0.5813 ms/step: the per-tile prologue / epilogue,
+// not the classes' 1 / 2 / 2 / 4 taps, sets the workgroups' length), so off by default
+inline int bal_enabled() {
+  static int on = env_flag("CV_BAL", 0);
+  return on;
 }
 inline int xcd_enabled() {
   static int on = env_flag("CV_XCD", 0);
@@ -461,6 +480,25 @@ int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
         long G = slots > (tiles + 1) / 2 ? slots : (tiles + 1) / 2;
         if (p.xcd) G = (G + 7) & ~7L;  // (tile w + G on the same XCD as tile w: the XCD-grouped order needs it)
         if (G > tiles) G = tiles;
+        p.bal_ncls = 0;
+        if (OP == OP_SCATTER && bal_enabled() && !p.xcd) {  // classes of unequal taps: K-balanced pairing
+          const int s = p.g.s, ncls = s * s;
+          int taps[4], ord[4];
+          bool uneq = false;
+          for (int c = 0; c < ncls && ncls <= 4; ++c) {
+            const int ry = c / s, rx = c % s;
+            taps[c] = ((p.g.kh > ry) ? (p.g.kh - ry + s - 1) / s : 0) * ((p.g.kw > rx) ? (p.g.kw - rx + s - 1) / s : 0);
+            ord[c] = c;
+            if (taps[c] != taps[0]) uneq = true;
+          }
+          if (uneq && ncls <= 4 && (int)grid.z == ncls) {
+            for (int i = 0; i < ncls; ++i)  // stable: heaviest first
+              for (int j = i + 1; j < ncls; ++j)
+                if (taps[ord[j]] > taps[ord[i]]) { const int q = ord[i]; ord[i] = ord[j]; ord[j] = q; }
+            p.bal_ncls = ncls;
+            for (int i = 0; i < ncls; ++i) p.cls_order[i] = ord[i];
+          }
+        }
         hipLaunchKernelGGL(kern2, dim3((unsigned)G), dim3(NT), lds, st, p);
         CV_LAUNCH_CHECK("gemm2");
         return 0;

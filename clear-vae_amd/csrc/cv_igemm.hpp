@@ -59,6 +59,11 @@ struct Args {
   // small-grid tile; GATHER: the N tiles of one M tile; WGRAD: the M tiles of one (N tile, K split)), so each
   // operand tile is fetched into one XCD's L2 once
   int xcd;
+  // two-tile SCATTER launch whose parity classes differ in K (stride 2, odd kernel: 1 / 2 / 2 / 4 taps): the
+  // slot -> tile permutation that balances the workgroups' K work (gemm_kernel2).  cls_order: the classes by
+  // taps, heaviest first; 0 classes: identity order
+  int bal_ncls;
+  int cls_order[4];
   // fast divisors (filled by finalize_divs at launch)
   FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
 };
