@@ -258,6 +258,8 @@ struct BwdArgs {
   double* gstat_out;    // the complete backward sums (sum dz, sum dz*xhat) go to replica 0 of [REPL][2][F]
   const float* z;       // [n][K] the Linear's input
   float* gw;            // [F][K] += dW
+  const float* w;       // [F][K] the Linear's weight (dz != nullptr)
+  float* dz;            // [n][K] += d(h) W over the workgroup's 16 features (fp32 atomics; caller zeroes), or nullptr
   int n, K, F, pix, ch;
 };
 
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   constexpr int P = KR + 4;
   const int K = A.K, n = A.n, F = A.F, nt = (n + 15) >> 4;
   float* sz = smem;                    // [nt * 16][P]
-  float* sred = smem + nt * 16 * P;    // [NW waves][DF][KR]: the weight-gradient fold
+  float* sred = smem + nt * 16 * P;    // [NW waves][DF][KR]: the weight-gradient fold, then [NW][16][17] transposes
   __shared__ double red[2][NTD / 64][DF];
   __shared__ double fs[2][DF];
   __shared__ BnFwdC kf[DF];
@@ -342,6 +344,19 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   f32x4 acc[KR / 16];
 #pragma unroll
   for (int j = 0; j < KR / 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // dz partials: B fragments W[f(col0 + 4 lq + s)][16 jt + lr]; the d(h) tile goes through a wave-private LDS
+  // transpose into the (row, feature) A fragment
+  f32x4 wz[KR / 16];
+  float* stp = sred + (size_t)NW * DF * KR + (size_t)w * 16 * 17;  // (past the fold area: waves end at different times)
+  if (A.dz) {
+#pragma unroll
+    for (int jt = 0; jt < KR / 16; ++jt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int fc = feature_of(col0 + 4 * lq + s, A.pix, A.ch), j = 16 * jt + lr;
+        wz[jt][s] = j < K ? A.w[(size_t)fc * K + j] : 0.f;
+      }
+  }
   for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
     float hv[TB][4], dv[TB][4];
     load(tile0, hv, dv);
@@ -359,6 +374,26 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
       }
       // dW^T tile: [k][col] += z[rows][k]^T d(h)[rows][col]
       mma_rows_t<KR>(sz, 16 * tile, dp, acc);
+      if (A.dz) {  // dz[rows][j] += sum over the 16 features d(h)[rows][f] W[f][j]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stp[(4 * lq + r) * 17 + lr] = dp[r];
+        __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
+        f32x4 at;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) at[s] = stp[lr * 17 + 4 * lq + s];
+#pragma unroll
+        for (int jt = 0; jt < KR / 16; ++jt) {
+          f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s], wz[jt][s], c, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * tile + 4 * lq + r, j = 16 * jt + lr;
+            if (row < n && j < K) atomicAdd(A.dz + (size_t)row * K + j, c[r]);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();  // (the next tile's transpose overwrites stp)
+      }
     }
   }
   // lane l holds dW[col lr][k = 16 jt + 4 lq + r]: fold the waves in order
@@ -724,9 +759,10 @@ extern "C" int cv_decoder_input_forward(const cv_linear* g, const float* heads, 
 }
 
 extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const float* h, const cv_bn* bn,
-                                         double* gstat_out, const float* z, float* gweight, cv_stream_t stream) {
+                                         double* gstat_out, const float* z, float* gweight, const float* weight,
+                                         float* dz, cv_stream_t stream) {
   clear_error();
-  CV_REQUIRE(g && ga && h && bn && z && gweight, "decoder_input_backward: null args");
+  CV_REQUIRE(g && ga && h && bn && z && gweight && (!dz || weight), "decoder_input_backward: null args");
   CV_REQUIRE(bn->train && bn->stat && g->out_features == bn->C && g->in_features % 2 == 0,
              "decoder_input_backward: BN1d must be train-mode with its forward sums, C = out_features");
   const int K = g->in_features, F = g->out_features;
@@ -739,6 +775,8 @@ extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const fl
   a.gstat_out = gstat_out;
   a.z = z;
   a.gw = gweight;
+  a.w = weight;
+  a.dz = dz;
   a.n = g->n;
   a.K = K;
   a.F = F;
@@ -746,7 +784,8 @@ extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const fl
   a.ch = g->out_ch;
   return pick_kr(K, [&](auto kr) -> int {
     constexpr int KR = decltype(kr)::value;
-    const size_t lds = ((size_t)((g->n + 15) & ~15) * (KR + 4) + (size_t)(NTD / 64) * DF * KR) * sizeof(float);
+    const size_t fold = (size_t)(NTD / 64) * (DF * KR + 16 * 17);  // the weight-gradient fold + the dz transposes
+    const size_t lds = ((size_t)((g->n + 15) & ~15) * (KR + 4) + fold) * sizeof(float);
     const void* kern = (const void*)declinear_bwd_kernel<KR>;
     if (set_lds(kern, lds)) {
       set_error("decoder_input_backward: LDS carve-out of %zu bytes refused", lds);

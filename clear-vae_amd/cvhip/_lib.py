@@ -209,7 +209,7 @@ _SIGS = {
     ),
     "cv_decoder_input_backward": (
         c_int,
-        [_P(cv_linear), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p],
+        [_P(cv_linear), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     "cv_heads_forward_supported": (c_int, [c_int, c_int, c_int, c_int]),
     "cv_heads_forward": (

@@ -804,10 +804,12 @@ class Workspace:
             self._wgrad_call(P, "conv", g, xin, gout, param_grad(c.mod.weight), None, ("dec", li), defer)
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
-        if self.fused_decoder_input():  # gah <- d(h) in place, weight gradient, BN1d backward sums
+        if self.fused_decoder_input():  # gah <- d(h) in place, weight gradient, BN1d backward sums, dz
+            if zero_dz:
+                P.add("cv_zero", dz_out, dz_out.numel() * 4)
             P.add("cv_decoder_input_backward", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
-                  self.z, param_grad(sp.dec_lin.weight))
-            gout = operand(self.gah)
+                  self.z, param_grad(sp.dec_lin.weight), sp.dec_lin.weight, dz_out)
+            return
         else:
             P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
                   self.z, param_grad(sp.dec_lin.weight))

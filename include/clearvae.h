@@ -219,15 +219,16 @@ int cv_declinear_backward_weight(const cv_linear* g, float* da, const float* h, 
  * cv_linear_forward + cv_bn_apply.
  * Backward (trainer.py:482 through vae.py:33-35): ga [n][F] = d(ReLU output) is overwritten with d(h) (ReLU
  * mask, then the BN1d backward transform); gstat_out replica 0 receives the complete backward sums; gweight
- * [F][2d] += d(h)^T z.  dz = d(h) W is left to cv_linear_backward_data (no transform).  Replaces the two
- * launches of cv_declinear_backward_weight.  Contract: cv_decoder_input_supported(n, d, F) (n*2d <= 16384,
+ * [F][2d] += d(h)^T z; with dz != NULL also dz [n][2d] += d(h) W (weight = the Linear's [F][2d]; each workgroup
+ * adds its 16 features' share with fp32 atomics, the caller zeroes dz), else dz is left to
+ * cv_linear_backward_data on d(h).  Replaces the two launches of cv_declinear_backward_weight (and the dz GEMM).  Contract: cv_decoder_input_supported(n, d, F) (n*2d <= 16384,
   * 2d <= 128, F % 16 == 0, d even). */
 int cv_decoder_input_supported(int n, int d, int features);
 int cv_decoder_input_forward(const cv_linear* g, const float* heads, const float* eps, uint64_t seed,
                              uint64_t* offset, float* z, const float* weight, const float* bias, const cv_bn* bn,
                              double* stat_out, float* h, float* ah, cv_stream_t stream);
 int cv_decoder_input_backward(const cv_linear* g, float* ga, const float* h, const cv_bn* bn, double* gstat_out,
-                              const float* z, float* gweight, cv_stream_t stream);
+                              const float* z, float* gweight, const float* weight, float* dz, cv_stream_t stream);
 
 /* Encoder heads forward in one launch (the four nn.Linear heads vae.py:27-30 over the Flatten of the last conv
  * block vae.py:25, its BatchNorm2d + ReLU applied to y on load): heads [n][4d] = ReLU(BN(y)) W^T + bias with W

@@ -60,7 +60,7 @@ for n, d, ch, pix in ((512, 8, 128, 16), (256, 32, 512, 4)):
 
     def bwd():
         return L.cv_decoder_input_backward(ctypes.byref(lin), ga.data_ptr(), h.data_ptr(), ctypes.byref(bn),
-                                           gstat.data_ptr(), z.data_ptr(), gw.data_ptr(), s)
+                                           gstat.data_ptr(), z.data_ptr(), gw.data_ptr(), W.data_ptr(), None, s)
 
     def rep():
         return L.cv_reparam_forward(heads.data_ptr(), n, d, None, ctypes.c_uint64(1), off.data_ptr(), z.data_ptr(),

@@ -95,8 +95,9 @@ def test_decoder_input_forward_backward(n, d, ch, pix):
     ga_pt = torch.tensor(g.standard_normal((n, F)), dtype=torch.float64, device=dev)
     ga = _storage(ga_pt, pix, ch).float().contiguous()
     gw = torch.zeros(F, K, device=dev)
+    dzo = torch.zeros(n, K, device=dev)
     _lib.call("cv_decoder_input_backward", ctypes.byref(lin), ga.data_ptr(), h.data_ptr(), ctypes.byref(bn),
-              gstat.data_ptr(), z.data_ptr(), gw.data_ptr(), s)
+              gstat.data_ptr(), z.data_ptr(), gw.data_ptr(), W.data_ptr(), dzo.data_ptr(), s)
     torch.cuda.synchronize()
     # the kernel's own ReLU decisions: the backward re-derives the forward's constants from the same sums, so
     # its mask is the forward's ah > 0
@@ -109,6 +110,7 @@ def test_decoder_input_forward_backward(n, d, ch, pix):
     assert _rel(gstat[0, 0], dz.sum(0)) < 1e-6 and _rel(gstat[0, 1], (dz * xhat).sum(0)) < 1e-5
     assert _rel(ga, _storage(dh, pix, ch)) < 1e-5
     assert _rel(gw, dh.T @ zd) < 1e-5
+    assert _rel(dzo, dh @ W.double()) < 1e-5
 
 
 def test_decoder_input_eval_and_given_z():
