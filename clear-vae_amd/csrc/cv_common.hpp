@@ -77,6 +77,9 @@ int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const floa
 int edge_wgrad(const Geo& g, const cv_operand* small, const cv_operand* big, float* gw, float* gbias, float* work,
                size_t work_bytes, hipStream_t st);
 size_t edge_wgrad_ws_bytes(const Geo& g, bool bias);
+int edge_scatter_out(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
+                     const cv_epilogue* ep, const cv_bn* obn, const float* x, float* xhat, double* rec_out, float* dv,
+                     double* gstat, const float* rec_scale, hipStream_t st);
 int edge_bwd(const Geo& g, const cv_operand* gout, const float* wg, float* gin, const cv_epilogue* ep,
              const cv_operand* x, float* gw, float* work, size_t work_bytes, hipStream_t st);
 

@@ -386,8 +386,25 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
 // (one contiguous NHWC range) together with the statistics epilogue.
 // (Round 2 ran this layer as per-class VALU dot products — 4x the FMAs' own instruction count issued,
 // ~54 us on the VAE64 layer; a col2im variant through LDS read-modify-writes measured 70 us.)
-template <int CB, int KK>
-__global__ __launch_bounds__(ET) void edge_scatter_kernel(const EArgs P) {
+// The decoder output (cv_output_loss: the output BatchNorm2d + Sigmoid, vae.py:44-45 / :154-155, the reconstruction
+// term and its backward seed, losses.py:41-47) fused behind the ConvT-to-image forward (OUT = true): every
+// workgroup publishes its band's BN sums, waits until all have (the host launches this form only when the whole
+// grid is resident at once; the wait is bounded, a timeout sets g_eo_sync[3] and proceeds), folds the output
+// BN's constants and turns its band — still in LDS — into x_hat, the reconstruction sum and dv, with the
+// arithmetic of output_loss_kernel.  The last workgroup out resets the counters.
+struct OArgs {
+  cv_bn bn;               // the output BatchNorm2d (this launch's statistics epilogue fills its sums)
+  const float* x;         // [n][CB][hb][wb] the input batch (NCHW)
+  float* xhat;            // NCHW
+  double* rec_out;        // [CV_REC_REPL] += sum (xhat - x)^2 / n
+  float* dv;              // NHWC backward seed (nullptr: forward only)
+  double* gstat;          // [REPL][2][CB] backward sums
+  const float* rec_scale;
+};
+__device__ unsigned g_eo_sync[4];  // [0] arrivals, [1] finishes, [3] timeout flag
+
+template <int CB, int KK, bool OUT>
+__global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EArgs P, const OArgs O) {
   constexpr int NCOL = 4 * CB;  // GEMM columns: class (2 cy + cx) * CB + output channel
   static_assert(NCOL <= 16 && KK <= 4, "one 16-column tile; taps cy + 2 - 2 dy < 4");
   __shared__ BnFwdC kf[CS];
@@ -504,6 +521,101 @@ __global__ __launch_bounds__(ET) void edge_scatter_kernel(const EArgs P) {
     }
   }
   if (mode == CV_STAT_FWD) stats_out<CB>(s1, s2, P.ep.stat_out, CB, red);
+  if constexpr (OUT) {
+    __shared__ BnFwdC ko[4];
+    __shared__ double ored[ET / 64][1 + 2 * 4];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned nblk = gridDim.x * gridDim.y;
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(g_eo_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int it = 0;
+      while (__hip_atomic_load(g_eo_sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nblk) {
+        __builtin_amdgcn_s_sleep(8);
+        if (++it > (1 << 20)) {
+          __hip_atomic_store(g_eo_sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (t < CB) {  // the output BN's constants from the replica sums (every workgroup's are in)
+      double a = 0.0, q = 0.0;
+      const int R = CV_STAT_REPL(CB);
+      for (int r = 0; r < R; ++r) {
+        a += __hip_atomic_load(O.bn.stat + (size_t)r * 2 * CB + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        q += __hip_atomic_load(O.bn.stat + (size_t)r * 2 * CB + CB + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ko[t] = bn_fwd_const_s(O.bn, t, a, q);
+    }
+    __syncthreads();
+    const float scale = (O.rec_scale ? O.rec_scale[0] : 1.0f) * 2.0f / (float)g.n;
+    float rec = 0.f, o1[CB], o2[CB];
+#pragma unroll
+    for (int j = 0; j < CB; ++j) { o1[j] = 0.f; o2[j] = 0.f; }
+    const size_t band0 = (size_t)(n * g.hb + yb0) * g.wb * CB;
+    for (int i = t; i < tot; i += ET) {
+      const int c = i % CB, pix = i / CB, yy = yb0 + pix / g.wb, xx = pix - (pix / g.wb) * g.wb;
+      const size_t nchw = ((size_t)(n * CB + c) * g.hb + yy) * g.wb + xx;
+      const float yv = sOut[i];
+      BnFwdC kk;
+#pragma unroll
+      for (int j = 0; j < CB; ++j)
+        if (j == c) kk = ko[j];
+      const float v = bn_out(yv, kk);
+      const float xh = 1.0f / (1.0f + expf(-v));
+      const float diff = xh - O.x[nchw];
+      O.xhat[nchw] = xh;
+      rec = fmaf(diff, diff, rec);
+      if (O.dv) {
+        const float dd = scale * diff * xh * (1.0f - xh);
+        O.dv[band0 + i] = dd;
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+          if (j == c) {
+            o1[j] += dd;
+            o2[j] += dd * ((yv - kk.mu) * kk.istd);
+          }
+      }
+    }
+    double vals[1 + 2 * CB];
+    vals[0] = (double)rec;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) { vals[1 + j] = (double)o1[j]; vals[1 + CB + j] = (double)o2[j]; }
+#pragma unroll
+    for (int q = 0; q < 1 + 2 * CB; ++q) {
+      const double v = wave_sum(vals[q]);
+      if (lane == 0) ored[w][q] = v;
+    }
+    __syncthreads();
+    if (t == 0) {
+      const unsigned blk = blockIdx.y * gridDim.x + blockIdx.x;
+      double r = 0.0;
+#pragma unroll
+      for (int ww = 0; ww < ET / 64; ++ww) r += ored[ww][0];
+      atomic_add_f64(O.rec_out + blk % CV_REC_REPL, r / (double)g.n);
+      if (O.dv) {
+        const int repl = blk % CV_STAT_REPL(CB);
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+          double a = 0.0, bq = 0.0;
+#pragma unroll
+          for (int ww = 0; ww < ET / 64; ++ww) {
+            a += ored[ww][1 + j];
+            bq += ored[ww][1 + CB + j];
+          }
+          atomic_add_f64(O.gstat + (size_t)repl * 2 * CB + j, a);
+          atomic_add_f64(O.gstat + (size_t)repl * 2 * CB + CB + j, bq);
+        }
+      }
+      if (__hip_atomic_fetch_add(g_eo_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
+        __hip_atomic_store(g_eo_sync + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g_eo_sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- weight gradient (split partials)
@@ -903,8 +1015,35 @@ int edge_gather(const Geo& g, const cv_operand* in, const float* wg, const float
   return launch(kern, dim3(cdiv(g.hs, a.rows), g.n), lds, a, st, "edge_gather");
 }
 
+static int edge_scatter_impl(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
+                             const cv_epilogue* ep, const OArgs* o, hipStream_t st);
+
 int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
                  const cv_epilogue* ep, hipStream_t st) {
+  return edge_scatter_impl(g, in, ws, bias, out, ep, nullptr, st);
+}
+
+// the ConvT-to-image forward with the decoder output fused (OArgs); -1 when not applicable (then the caller runs
+// edge_scatter and cv_output_loss)
+int edge_scatter_out(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
+                     const cv_epilogue* ep, const cv_bn* obn, const float* x, float* xhat, double* rec_out, float* dv,
+                     double* gstat, const float* rec_scale, hipStream_t st) {
+  if (!ep || ep->stat_mode != CV_STAT_FWD || !obn || !obn->train || obn->C != g.cb || obn->stat != ep->stat_out ||
+      !x || !xhat || !rec_out || (dv && !gstat))
+    return -1;
+  OArgs o;
+  o.bn = *obn;
+  o.x = x;
+  o.xhat = xhat;
+  o.rec_out = rec_out;
+  o.dv = dv;
+  o.gstat = gstat;
+  o.rec_scale = rec_scale;
+  return edge_scatter_impl(g, in, ws, bias, out, ep, &o, st);
+}
+
+static int edge_scatter_impl(const Geo& g, const cv_operand* in, const float* ws, const float* bias, float* out,
+                             const cv_epilogue* ep, const OArgs* o, hipStream_t st) {
   // (the statistics epilogue of this layer is the forward one: the decoder's output BatchNorm)
   if (!geo_ok(g) || g.s != 2 || (g.hb & 1) || (g.wb & 1) || !ep_ok(ep, g.cb)) return -1;
   if (ep && ep->stat_mode == CV_STAT_BWD) return -1;
@@ -948,8 +1087,42 @@ int edge_scatter(const Geo& g, const cv_operand* in, const float* ws, const floa
   if (lds < pre) lds = pre;
   if (lds > 96 * 1024) return -1;
   const void* kern = nullptr;
-  CV_EDGE_PICK(edge_scatter_kernel);
-  return launch(kern, dim3(cdiv(nby, rb), g.n), lds, a, st, "edge_scatter");
+  const dim3 grid(cdiv(nby, rb), g.n);
+  OArgs oa;
+  memset(&oa, 0, sizeof(oa));
+  if (o) {
+    CV_EDGE_PICK(edge_scatter_kernel, , true);
+    // every workgroup resident at once (half the device's slots: margin for other streams' kernels)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = -1;
+      (void)hipGetLastError();
+    }
+    int occ = 0;
+    if (!kern || set_lds(kern, lds) || cus <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, ET, lds) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1;
+    }
+    if ((long)grid.x * grid.y > (long)occ * cus / 2) return -1;
+    oa = *o;
+  } else {
+    CV_EDGE_PICK(edge_scatter_kernel, , false);
+  }
+  if (set_lds(kern, lds)) {
+    set_error("edge_scatter: LDS carve-out of %zu bytes refused", lds);
+    return 1;
+  }
+  EArgs arg = a;
+  void* params[] = {&arg, &oa};
+  if (hipLaunchKernel(kern, grid, dim3(ET), params, lds, st) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("edge_scatter: launch failed");
+    return 2;
+  }
+  return 0;
 }
 
 

@@ -1039,6 +1039,18 @@ static int gather_split(long tiles, int ktiles) {
 }
 
 // GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
+// CV_FUSED_OUT=1: the ConvT-to-image forward and the decoder output in one launch with a grid-wide wait for the
+// output BN's sums (edge_scatter_out); measured slower (MNIST 0.582 -> 0.616 ms/step: the fused launch needs a
+// 4-workgroups-per-CU register budget to be co-resident and ran 57.6 us against 16 + 9.7 us), so off by default
+static int fused_out_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CV_FUSED_OUT");
+    on = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return on;
+}
+
 static int run_gather(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                       const cv_epilogue* ep, hipStream_t st, const char* what, int mma) {
   if (!g_force_generic) {
@@ -1428,6 +1440,28 @@ extern "C" int cv_conv_backward_weight_deferred(const cv_conv* g, const cv_opera
   const int r = cv_conv_backward_weight(g, in, gout, gweight, gbias, 0, work, work_bytes, stream);
   g_defer_sink = nullptr;
   return r;
+}
+
+extern "C" int cv_output_loss(const cv_bn* bn, const float* y, const float* x, int n, int c, int hw, float* xhat,
+                              double* rec_out, float* dv_out, double* gstat_out, const float* rec_scale,
+                              cv_stream_t stream);
+
+extern "C" int cv_convt_output_loss(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* bias,
+                                    float* y, const cv_epilogue* ep, const cv_bn* bn, const float* x, float* xhat,
+                                    double* rec_out, float* dv_out, double* gstat_out, const float* rec_scale,
+                                    cv_stream_t stream) {
+  clear_error();
+  if (check_conv(g) || check_operand(in, "convT_output_loss")) return 1;
+  CV_REQUIRE(wpacked && y && bn && x && xhat && rec_out, "convT_output_loss: null args");
+  if (g->transposed && !g_force_generic && fused_out_enabled()) {
+    const int r = edge_scatter_out(geo_of(g), in, wpacked, bias, y, ep, bn, x, xhat, rec_out, dv_out, gstat_out,
+                                   rec_scale, S(stream));
+    if (r >= 0) return r;
+  }
+  const int r = cv_conv_forward(g, in, wpacked, bias, y, ep, stream);
+  if (r) return r;
+  return cv_output_loss(bn, y, x, g->n, g->c_out, g->h_out * g->w_out, xhat, rec_out, dv_out, gstat_out, rec_scale,
+                        stream);
 }
 
 extern "C" int cv_conv_backward_deferred(const cv_conv* g, const cv_operand* gout, const float* wpacked, float* gin,

@@ -825,6 +825,240 @@ __global__ __launch_bounds__(256) void ntxent_grad_lds_kernel(const NtArgs A) {
   }
 }
 
+// ---------------------------------------------------------------- NT-Xent rows + gradients in one launch
+// (A/B knob CV_NT_FUSED=1; measured slower than the two launches — MNIST latent step 35.2 -> 42.2 us in-step: the
+// wait holds every workgroup at the slowest one's log-sum-exps and the polling adds its own latency — so off.)
+// The gradient of row i needs the log-sum-exps of every row j (the loss is symmetric in S), so the two passes
+// above are two launches.  Here each workgroup computes its rows' log-sum-exps, publishes them (release, then an
+// arrival count per branch), waits until every workgroup of its branch and the latent-combine workgroup have
+// arrived (acquire), and runs the gradient pass for the same rows.  The host takes this path only when the whole
+// grid fits the device's resident slots at once (occupancy query), so every awaited workgroup is running; the
+// wait is bounded all the same (~0.1 s: a timeout sets g_nt_sync[7] and proceeds rather than hanging).  The last
+// workgroup to finish resets the counters for the next launch (graph replays need no host zeroing).
+__device__ unsigned g_nt_sync[8];  // [0..1] branch arrivals, [2] combine done, [3] grad finishes, [7] timeout flag
+
+__device__ __forceinline__ unsigned nt_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void ntxent_fused_kernel(const NtArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char ntl_smem[];
+  __shared__ float scratch[16];
+  __shared__ double dscratch[16];
+  const int t = threadIdx.x;
+  if (blockIdx.y >= (unsigned)A.nbr) {  // the latent combine (KL + decoder chain seed of dheads)
+    if (A.with_combine && blockIdx.x == 0) {
+      combine_body<256>(A.cmb, reinterpret_cast<double*>(ntl_smem));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every wave's dheads stores complete before the release)
+      __syncthreads();
+      if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(g_nt_sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
+  const int br = blockIdx.y;
+  const Branch& b = A.br[br];
+  const int n = A.n, d = A.d;
+  const bool cosine = A.sim == CV_SIM_COSINE;
+  const bool need_lv = !(A.sim == CV_SIM_COSINE || A.sim == CV_SIM_L2);
+  NtLds L = ntl_carve(ntl_smem, n, d, need_lv, true);
+  ntl_stage(b, A.label, n, d, need_lv, cosine, true, L);  // (its lse copy is stale: reloaded below)
+  const int lane = t & 63, w = t >> 6;
+  const int iend = min(n, (int)(blockIdx.x + 1) * A.rpb);
+  // ---- rows: log-sum-exps (ntxent_rows_lds_kernel's loop)
+  for (int i = blockIdx.x * A.rpb + w; i < iend; i += 4) {
+    float mi[DM], li[DM], mj[DM], lj[DM];
+    ntl_theta<DM>(L, i, d, mi, li, need_lv);
+    const long long lab = L.lab[i];
+    float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
+    for (int j = lane; j < n; j += 64) {
+      if (j == i) continue;
+      ntl_theta<DM>(L, j, d, mj, lj, need_lv);
+      const float S = cosine ? dot_u<DM>(mi, mj, d) : sim_ij<DM>(A.sim, mi, li, 1.f, mj, lj, 1.f, d);
+      const float sv = S / A.tau;
+      lse_merge(ma, sa, sv, 1.f);
+      const bool pos = b.ps ? (L.lab[j] != lab) : (L.lab[j] == lab);
+      if (pos) lse_merge(mp, sp, sv, 1.f);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(ma, o, 64), s2 = __shfl_xor(sa, o, 64);
+      const float m3 = __shfl_xor(mp, o, 64), s3 = __shfl_xor(sp, o, 64);
+      lse_merge(ma, sa, m2, s2);
+      lse_merge(mp, sp, m3, s3);
+    }
+    if (lane == 0) {
+      b.lse[i] = (sa > 0.f) ? ma + logf(sa) : -INFINITY;
+      b.lse[n + i] = (sp > 0.f) ? mp + logf(sp) : -INFINITY;
+    }
+  }
+  // ---- publish, wait for the branch's other workgroups and the combine
+  __shared__ int timed_out;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(g_nt_sync + br, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = gridDim.x, wantc = A.with_combine ? 1u : 0u;
+    int it = 0;
+    while (nt_load(g_nt_sync + br) < want || nt_load(g_nt_sync + 2) < wantc) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++it > (1 << 20)) {
+        __hip_atomic_store(g_nt_sync + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    timed_out = it > (1 << 20);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  for (int j = t; j < 2 * n; j += 256) L.lse[j] = __hip_atomic_load(b.lse + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  // ---- gradients (ntxent_grad_lds_kernel's body)
+  float cnt = 0.f;
+  double lsum = 0.0;
+  for (int j = t; j < n; j += 256) {
+    const float l = L.lse[j] - L.lse[n + j];
+    if (isfinite(l)) {
+      cnt += 1.f;
+      lsum += (double)l;
+    }
+  }
+  const float nf = block_sum<256>(cnt, scratch);
+  if (blockIdx.x == 0) {
+    const double tot = block_sum<256>(lsum, dscratch);
+    if (t == 0 && b.loss_out) b.loss_out[0] = (nf > 0.f) ? (float)(tot / (double)nf) : NAN;
+  }
+  if (b.dmu) {
+    const float gup = b.gmul * (b.gscale ? b.gscale[0] : 1.0f);
+    const float c = (nf > 0.f) ? gup / (nf * A.tau) : 0.f;
+    for (int i = blockIdx.x * A.rpb + w; i < iend; i += 4) {
+      float mi[DM], li[DM], mj[DM], lj[DM], gm[DM], gl[DM];
+      ntl_theta<DM>(L, i, d, mi, li, need_lv);
+#pragma unroll
+      for (int k = 0; k < DM; ++k) { gm[k] = 0.f; gl[k] = 0.f; }
+      const float ni = cosine ? L.nrm[i] : 1.f;
+      const bool clamped_i = cosine && !(L.raw[i] > 1e-8f);
+      const long long lab = L.lab[i];
+      const float la_i = L.lse[i], lp_i = L.lse[n + i];
+      const bool fin_i = isfinite(la_i - lp_i);
+      for (int j = lane; j < n; j += 64) {
+        if (j == i) continue;
+        ntl_theta<DM>(L, j, d, mj, lj, need_lv);
+        const float S = cosine ? dot_u<DM>(mi, mj, d) : sim_ij<DM>(A.sim, mi, li, 1.f, mj, lj, 1.f, d);
+        const float sv = S / A.tau;
+        const bool pos = b.ps ? (L.lab[j] != lab) : (L.lab[j] == lab);
+        const float la_j = L.lse[j], lp_j = L.lse[n + j];
+        const bool fin_j = isfinite(la_j - lp_j);
+        float G = 0.f;
+        if (fin_i) G += c * (expf(sv - la_i) - (pos ? expf(sv - lp_i) : 0.f));
+        if (fin_j) G += c * (expf(sv - la_j) - (pos ? expf(sv - lp_j) : 0.f));
+        if (G != 0.f) {
+          if (cosine) {
+#pragma unroll
+            for (int k = 0; k < DM; ++k)
+              if (k < d) gm[k] += G * (clamped_i ? mj[k] : (mj[k] - S * mi[k]));
+          } else {
+            sim_grad_row<DM>(A.sim, mi, li, 1.f, false, mj, lj, 1.f, S, G, d, gm, gl);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < DM; ++k) {
+        if (k < d) {
+          gm[k] = wave_sum(gm[k]);
+          if (cosine) gm[k] = gm[k] / ni;
+          if (need_lv) gl[k] = wave_sum(gl[k]);
+        }
+      }
+      float om = 0.f, ol = 0.f;
+#pragma unroll
+      for (int k = 0; k < DM; ++k)
+        if (k == lane) { om = gm[k]; ol = need_lv ? gl[k] : 0.f; }
+      if (lane < d) {
+        float* pm = b.dmu + (size_t)i * b.gld + lane;
+        *pm = A.accumulate ? *pm + om : om;
+        if (b.dlv) {
+          float* pl = b.dlv + (size_t)i * b.gld + lane;
+          *pl = A.accumulate ? *pl + ol : ol;
+        }
+      }
+    }
+  }
+  // ---- the last workgroup out resets the counters for the next launch
+  __syncthreads();
+  if (t == 0) {
+    const unsigned tot = (unsigned)A.nbr * gridDim.x;
+    if (__hip_atomic_fetch_add(g_nt_sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tot - 1) {
+      __hip_atomic_store(g_nt_sync + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g_nt_sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g_nt_sync + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g_nt_sync + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  (void)timed_out;
+}
+
+// fraction of the device's resident slots the fused grid may use (CV_NT_FILL, percent; default 100)
+static double nt_fused_fill() {
+  static double f = -1.0;
+  if (f < 0) {
+    const char* e = getenv("CV_NT_FILL");
+    f = e ? atof(e) / 100.0 : 1.0;
+  }
+  return f;
+}
+
+// one launch for rows + gradients when the whole grid is resident at once; -1 otherwise
+static int ntxent_launch_fused(const NtArgs& a, int nbr, hipStream_t st) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("CV_NT_FUSED");  // measured slower (MNIST latent step 35.2 -> 42.2 us): off by default
+    mode = e ? atoi(e) : 0;
+  }
+  if (!mode) return -1;
+  const bool need_lv = !(a.sim == CV_SIM_COSINE || a.sim == CV_SIM_L2);
+  size_t lds = ntl_bytes(a.n, a.d, need_lv, true);
+  if (lds > 144 * 1024) return -1;
+  if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
+  NtArgs arg = a;
+  arg.rpb = NTL_ROWS;
+  arg.nbr = nbr;
+  const dim3 grid(cdiv(a.n, arg.rpb), nbr + (a.with_combine ? 1 : 0));
+  const void* kern;
+  if (a.d <= 8) kern = (const void*)ntxent_fused_kernel<8>;
+  else if (a.d <= 16) kern = (const void*)ntxent_fused_kernel<16>;
+  else if (a.d <= 32) kern = (const void*)ntxent_fused_kernel<32>;
+  else kern = (const void*)ntxent_fused_kernel<64>;
+  if (lds > 64 * 1024 && hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  // every workgroup must be resident at once (half the device's slots, for the margin of other streams' kernels)
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = -1;
+    (void)hipGetLastError();
+  }
+  int occ = 0;
+  if (cus <= 0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  if ((long)grid.x * grid.y > (long)occ * cus * nt_fused_fill()) return -1;
+  void* params[] = {&arg};
+  if (hipLaunchKernel(kern, grid, dim3(256), params, lds, st) != hipSuccess) {
+    ::cv::set_error("ntxent_fused: launch failed");
+    return 2;
+  }
+  return 0;
+}
+
 template <template <int> class K>
 struct DDispatch;
 
@@ -1030,8 +1264,11 @@ extern "C" int cv_latent_step(const float* heads, const float* z, const float* d
                "latent_step: branch %d gradient must land in dheads", i);
   a.with_combine = 1;
   a.cmb = CombineArgs{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses};
-  // launch 1: row log-sum-exps of every branch + the KL / decoder-chain seed of dheads (independent);
-  // launch 2: contrastive losses and their gradients accumulated into dheads
+  // one launch when its grid is resident at once (ntxent_fused_kernel), else launch 1: row log-sum-exps of every
+  // branch + the KL / decoder-chain seed of dheads (independent); launch 2: contrastive losses and their gradients
+  // accumulated into dheads
+  const int f = ntxent_launch_fused(a, nbr, S(stream));
+  if (f >= 0) return f;
   if (ntxent_launch(a, nbr, true, S(stream))) return 2;
   if (ntxent_launch(a, nbr, false, S(stream))) return 2;
   return 0;

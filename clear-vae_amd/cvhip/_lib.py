@@ -231,6 +231,11 @@ _SIGS = {
         [_P(cv_bn), c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p],
     ),
+    "cv_convt_output_loss": (
+        c_int,
+        [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), _P(cv_bn), c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "cv_output_backward": (
         c_int,
         [_P(cv_bn), c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

@@ -668,7 +668,8 @@ class Workspace:
     def forward_program(self, x: torch.Tensor, train: bool, eps=None, seed: int = 0, offset=None,
                         output: str = "xhat", rec_scale=None) -> Program:
         """Encoder + heads + reparam + decoder (+ running statistics).  output: 'xhat'
-        (cv_output_forward), 'loss' (cv_output_loss with backward seed), 'none' (statistics only)."""
+        (cv_output_forward), 'loss' (cv_convt_output_loss: the last ConvT + cv_output_loss with the backward seed),
+        'none' (statistics only)."""
         P = Program()
         if train:
             P.add("cv_zero", self.stats, self.stats.numel() * 8)
@@ -768,20 +769,21 @@ class Workspace:
             P.add("cv_linear_forward", lin, operand(z), sp.dec_lin.weight, sp.dec_lin.bias, self.h, 0, ep)
             P.add("cv_bn_apply", self.bn_1d.cv(train), self.h, self.ah, n, sp.dec_lin.out_features, Hu * Wu, Cu, 1)
         cur = self.ah
+        last = sp.dec[-1]
+        hw = last.h_out * last.w_out
         for li, c in enumerate(sp.dec):
             g = c.geom(n)
             op = operand(cur) if li == 0 else operand(cur, XF_BNRELU, self.bn_dec[li - 1].cv(train))
             ep = ep_fwd(self.bn_dec[li]) if train else ep_none()
+            if li == len(sp.dec) - 1 and output == "loss":  # the last ConvT and the output / loss seed together
+                assert train
+                P.add("cv_convt_output_loss", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep, self.bn_dec[-1].cv(True), x,
+                      self.xhat, self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
+                return
             P.add("cv_conv_forward", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep)
             cur = self.y_dec[li]
-        last = sp.dec[-1]
-        hw = last.h_out * last.w_out
         if output == "xhat":
             P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)
-        elif output == "loss":
-            assert train
-            P.add("cv_output_loss", self.bn_dec[-1].cv(True), cur, x, n, sp.in_ch, hw, self.xhat,
-                  self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
 
     def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True, defer=None):
         """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to

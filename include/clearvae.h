@@ -274,6 +274,14 @@ int cv_output_forward(const cv_bn* bn, const float* y, int n, int c, int hw, flo
 int cv_output_loss(const cv_bn* bn, const float* y, const float* x, int n, int c, int hw,
                    float* xhat, double* rec_out, float* dv_out, double* gstat_out,
                    const float* rec_scale, cv_stream_t stream);
+/* The last ConvTranspose2d (vae.py:43 / :153) and cv_output_loss in one call: y = convT(T(in)) + bias with its
+ * output BatchNorm's sums (ep, CV_STAT_FWD into bn->stat), then the decoder output, the reconstruction term and
+ * its backward seed exactly as cv_output_loss.  One launch when the edge kernel serves the layer and its whole
+ * grid is resident at once (the workgroups meet at a bounded grid-wide wait for the BN sums); else the two
+ * calls. */
+int cv_convt_output_loss(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* bias, float* y,
+                         const cv_epilogue* ep, const cv_bn* bn, const float* x, float* xhat, double* rec_out,
+                         float* dv_out, double* gstat_out, const float* rec_scale, cv_stream_t stream);
 /* backward of xhat = sigmoid(BN(y)) given dxhat (NCHW): dv (NHWC) + BN backward sums. */
 int cv_output_backward(const cv_bn* bn, const float* y, const float* xhat, const float* dxhat,
                        int n, int c, int hw, float* dv_out, double* gstat_out, cv_stream_t stream);
