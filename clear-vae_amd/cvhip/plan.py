@@ -163,16 +163,19 @@ def vae_spec(vae: nn.Module, image_hw: int | None = None) -> VaeSpec:
 class ParamArena:
     """All parameters of a module as views into one flat fp32 buffer (+ a flat gradient buffer)."""
 
-    def __init__(self, params: list, device):
+    def __init__(self, params: list, device, tight=()):
         self.params = list(params)
         self.device = torch.device(device)
         # every parameter starts on a 16-byte boundary (float4 loads); the gaps stay zero and get zero
-        # gradients, so Adam leaves them at zero
+        # gradients, so Adam leaves them at zero.  `tight`: parameters followed directly by the next one (a group
+        # the kernels address as one tensor: the four head weights [4d][F] and the four head biases [4d], whose
+        # d-element biases would otherwise be padded apart when d % 4 != 0)
+        tight = {id(p) for p in tight}
         self.offset = {}
         o = 0
         for p in self.params:
             self.offset[id(p)] = (o, p.numel())
-            o = (o + p.numel() + 3) & ~3
+            o = o + p.numel() if id(p) in tight else (o + p.numel() + 3) & ~3
         self.numel = o
         self.flat = torch.zeros(o, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(o, dtype=torch.float32, device=self.device)
@@ -234,7 +237,8 @@ def ensure_arena(vae: nn.Module, spec_fn=None):
         raise RuntimeError(
             "clear-vae_amd runs on MI355X (ROCm device 'cuda'); move the model with .to('cuda') first"
         )
-    arena = ParamArena(vae_param_order(vae, spec), dev)
+    arena = ParamArena(vae_param_order(vae, spec), dev,
+                       tight=[h.weight for h in spec.heads[:-1]] + [h.bias for h in spec.heads[:-1]])
     attach_packed(spec, dev)
     vae._cv_arena = arena
     vae._cv_spec = spec

@@ -1,0 +1,74 @@
+"""The fused step with each of this round's fused launches switched off (the A/B paths the engine also takes when a
+shape is outside a fused kernel's contract) and at shapes outside the contracts, against the fp64 oracle with the
+bars of test_gpu_parity.py:
+
+  * Workspace.FUSED_DECIN / FUSED_HEADS / FUSED_HEADS_FWD / FUSED_EDGE_BWD = False: the separate reparameterisation,
+    DENSE GEMMs, BN1d apply, mask / weight-gradient launches and the two edge backward launches;
+  * n = 1100 (n x 2d > the decoder-input kernel's LDS budget, so the engine falls back on its own) and z = 12 / 20
+    (d = 6 / 10 are not heads-forward column groups: the DENSE heads, the reparameterisation in the decoder-input
+    launch).  These latent widths also pin the arena layout: the four head biases are one [4d] vector to every
+    kernel, so they are packed without the per-parameter 16-byte padding (with it, d % 4 != 0 put biases 2-4 and
+    their gradients off by the padding: kl_c 0.7418 vs 0.7377 at z = 12 before the fix).
+
+Reference: the reference's CLEARVAETrainer._train step (code/src/trainer.py:447-484) restated by oracle/cpu_ref.py."""
+
+import pytest
+import torch
+
+from test_gpu_parity import LOSS_TOL, _check_grads, _fused_trainer
+
+pytestmark = pytest.mark.gpu
+
+KNOBS = ["FUSED_DECIN", "FUSED_HEADS", "FUSED_HEADS_FWD", "FUSED_EDGE_BWD"]
+
+
+def _run(n, zt, off, seed=5):
+    from oracle import cpu_ref as R
+    from cvhip import rng
+    from cvhip.engine import ClearStep
+    from cvhip.plan import Workspace
+
+    saved = {k: getattr(Workspace, k) for k in KNOBS}
+    try:
+        for k in off:
+            setattr(Workspace, k, False)
+        arch, C = "VAE", 1
+        sd = R.det_state(arch, zt, C)
+        x, label, ec, es, _ = R.det_inputs(n, C, 28, zt, 10, seed=seed)
+        hp = {"temperature": 0.1, "alpha": 100.0, "beta": 0.125, "ps": True, "loc": 0, "scale": 1}
+        tr = _fused_trainer(arch, zt, C, sd, hp)
+        eng = ClearStep.build(tr, "clear")
+        assert eng is not None
+        rng.clear_injections()
+        rng.inject_noise([torch.tensor(ec, dtype=torch.float32), torch.tensor(es, dtype=torch.float32)])
+        losses = eng.step(torch.tensor(x, dtype=torch.float32, device="cuda"),
+                          torch.tensor(label, device="cuda")).clone().cpu()
+        torch.cuda.synchronize()
+        o = R.clear_step(R.to_torch(sd), torch.tensor(x), torch.tensor(label), torch.tensor(ec), torch.tensor(es),
+                         arch, hp)
+        got = {"rec": float(losses[0]), "kl_c": float(losses[1]), "kl_s": float(losses[2]),
+               "c_loss": float(losses[3]), "s_loss": float(losses[4])}
+        for k, v in got.items():
+            assert abs(v - float(o[k])) <= LOSS_TOL * max(abs(float(o[k])), 1e-3), (k, v, float(o[k]))
+        _check_grads({k: p.grad for k, p in tr.model.named_parameters()}, o["grads"], arch)
+    finally:
+        for k, v in saved.items():
+            setattr(Workspace, k, v)
+
+
+@pytest.mark.parametrize("off", [KNOBS, ["FUSED_DECIN"], ["FUSED_HEADS_FWD"], ["FUSED_HEADS", "FUSED_EDGE_BWD"]],
+                         ids=lambda v: "+".join(v))
+def test_unfused_paths_match_oracle(off):
+    _run(64, 16, off)
+
+
+@pytest.mark.parametrize("n,zt", [(1100, 16), (64, 12), (64, 20)])
+def test_out_of_contract_shapes_match_oracle(n, zt):
+    from cvhip import _lib
+
+    d = zt // 2
+    if n == 1100:
+        assert _lib.lib().cv_decoder_input_supported(n, d, 2048) == 0
+    else:
+        assert _lib.lib().cv_heads_forward_supported(n, 2048, 128, d) == 0
+    _run(n, zt, [])
