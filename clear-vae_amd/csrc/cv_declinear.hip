@@ -490,12 +490,22 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
       mma_rows_t<JR>(sd, 16 * tile, a, acc);
     }
   }
-  // head biases: workgroup 0, one thread per head output
+  // head biases: workgroup 0 sums the staged dheads columns, NTD / JR row groups per column (a serial walk of n
+  // rows per column by JR threads was this launch's tail), folded in LDS in group order
+  __shared__ float gbr[NTD];
   if (blockIdx.x == 0 && A.gb) {
-    for (int j = t; j < J; j += NTD) {
-      float v = 0.f;
-      for (int r = 0; r < n; ++r) v += sd[r * P + j];
-      A.gb[j] += v;
+    constexpr int RG = NTD / JR;
+    const int j = t % JR, rgp = t / JR;
+    float v = 0.f;
+    if (j < J)
+      for (int r = rgp; r < n; r += RG) v += sd[r * P + j];
+    gbr[t] = v;
+    __syncthreads();
+    if (t < J) {
+      float u = 0.f;
+#pragma unroll
+      for (int q = 0; q < RG; ++q) u += gbr[q * JR + t];
+      A.gb[t] += u;
     }
   }
   s1 = col_fold(s1);

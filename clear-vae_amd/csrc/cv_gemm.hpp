@@ -400,6 +400,17 @@ inline int env_flag(const char* name, int dflt) {
 // CV_BAL=1: the two-tile SCATTER launches pair their tiles K-balanced (Args::bal_ncls) instead of w and w + G
 // in class-major order; measured neutral (MNIST 0.5802 vs 0.5813 ms/step: the per-tile prologue / epilogue,
 // not the classes' 1 / 2 / 2 / 4 taps, sets the workgroups' length), so off by default
+// deep ring when the launch's tiles fill at most num/den of one round of resident slots (CV_DEEP_FILL=<percent>,
+// default 50: "less than half a round")
+inline long deep_num() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_DEEP_FILL");
+    v = e ? atol(e) : 50;
+  }
+  return v;
+}
+inline long deep_den() { return 100; }
 inline int bal_enabled() {
   static int on = env_flag("CV_BAL", 0);
   return on;
@@ -455,7 +466,7 @@ int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
   if constexpr ((OP == OP_GATHER || OP == OP_SCATTER) && MT == MMA_F32 && DEPTH < CV_FAST_DEPTH_DEEP) {
     const long tiles = (long)grid.x * grid.y * grid.z;
     const long slots1 = deep_enabled() ? resident_slots((const void*)kern, lds) : 0;
-    if (slots1 > 0 && 2 * tiles <= slots1) {
+    if (slots1 > 0 && tiles * deep_den() <= slots1 * deep_num()) {
       auto kern4 = gemm_kernel<OP, BM, BN, XA, XB, EPI, CV_FAST_DEPTH_DEEP, MT>;
       if (carve((const void*)kern4)) return 1;
       hipLaunchKernelGGL(kern4, grid, dim3(NT), lds, st, a);
