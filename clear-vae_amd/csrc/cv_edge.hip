@@ -89,37 +89,56 @@ __device__ __forceinline__ float xf_apply(int xf, float x, float y, int c, const
   return x;
 }
 
-// Stage rows [yb0, yb0+NR) x cols [xb0, xb0+NC) x CB of image n of the big-grid operand, transformed,
-// zero outside the image, as dst[(rr*NC + cc)*CB + c].  8 loads in flight per thread.
-template <int CB>
-__device__ __forceinline__ void stage_big(const Geo& g, const cv_operand& o, int n, int yb0, int xb0, int NR, int NC,
-                                          const BnFwdC* kf, const BnBwdC* kb, float* dst) {
-  constexpr int U = 16;  // (VAE64 gather band: 14 elements per thread in one round trip)
+constexpr int BU = 16;  // elements of x (and y) per thread per batch of stage_big (VAE64 gather band: 14)
+// one batch of stage_big's loads from element `base` (zero outside the image; ok = inside)
+template <int CB, bool Y = true>
+__device__ __forceinline__ void big_load(const Geo& g, const cv_operand& o, int n, int yb0, int xb0, int NR, int NC,
+                                         int base, float (&v)[BU], float* yv) {
   const int tot = NR * NC * CB;
   const FDiv fnc = FDiv::make(NC);
-  for (int base = threadIdx.x; base < tot; base += ET * U) {
-    float v[U], yv[U];
-    bool ok[U];
 #pragma unroll
-    for (int q = 0; q < U; ++q) {
+  for (int q = 0; q < BU; ++q) {
+    const int i = base + q * ET;
+    const int c = i % CB, rc = i / CB;
+    const int rr = fnc.div(rc), cc = rc - rr * NC;
+    const int yb = yb0 + rr, xb = xb0 + cc;
+    v[q] = 0.f;
+    if (Y) yv[q] = 0.f;
+    if (i < tot && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb) {
+      const size_t off = o.nchw ? ((size_t)(n * CB + c) * g.hb + yb) * g.wb + xb
+                                : ((size_t)(n * g.hb + yb) * g.wb + xb) * CB + c;
+      v[q] = o.x[off];
+      if (Y && o.xf == CV_XF_BNBWD) yv[q] = o.y[off];
+    }
+  }
+}
+// Stage rows [yb0, yb0+NR) x cols [xb0, xb0+NC) x CB of image n of the big-grid operand, transformed,
+// zero outside the image (the conv's zero padding of the transformed tensor), as dst[(rr*NC + cc)*CB + c].
+// PRE: the first batch was requested earlier (big_load at base = threadIdx.x into pv / py).
+template <int CB, bool PRE = false>
+__device__ __forceinline__ void stage_big(const Geo& g, const cv_operand& o, int n, int yb0, int xb0, int NR, int NC,
+                                          const BnFwdC* kf, const BnBwdC* kb, float* dst, const float* pv = nullptr,
+                                          const float* py = nullptr) {
+  const int tot = NR * NC * CB;
+  const FDiv fnc = FDiv::make(NC);
+  for (int base = threadIdx.x; base < tot; base += ET * BU) {
+    float v[BU], yv[BU];
+    if (PRE && base == (int)threadIdx.x) {
+#pragma unroll
+      for (int q = 0; q < BU; ++q) {
+        v[q] = pv[q];
+        yv[q] = py ? py[q] : 0.f;
+      }
+    } else {
+      big_load<CB>(g, o, n, yb0, xb0, NR, NC, base, v, yv);
+    }
+#pragma unroll
+    for (int q = 0; q < BU; ++q) {
       const int i = base + q * ET;
       const int c = i % CB, rc = i / CB;
       const int rr = fnc.div(rc), cc = rc - rr * NC;
-      const int yb = yb0 + rr, xb = xb0 + cc;
-      ok[q] = i < tot && (unsigned)yb < (unsigned)g.hb && (unsigned)xb < (unsigned)g.wb;
-      v[q] = 0.f;
-      yv[q] = 0.f;
-      if (ok[q]) {
-        const size_t off = o.nchw ? ((size_t)(n * CB + c) * g.hb + yb) * g.wb + xb
-                                  : ((size_t)(n * g.hb + yb) * g.wb + xb) * CB + c;
-        v[q] = o.x[off];
-        if (o.xf == CV_XF_BNBWD) yv[q] = o.y[off];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < U; ++q) {
-      const int i = base + q * ET;
-      if (i < tot) dst[i] = ok[q] ? xf_apply(o.xf, v[q], yv[q], i % CB, kf, kb) : 0.f;
+      const bool ok = (unsigned)(yb0 + rr) < (unsigned)g.hb && (unsigned)(xb0 + cc) < (unsigned)g.wb;
+      if (i < tot) dst[i] = ok ? xf_apply(o.xf, v[q], yv[q], c, kf, kb) : 0.f;
     }
   }
 }
@@ -128,10 +147,32 @@ __device__ __forceinline__ void stage_big(const Geo& g, const cv_operand& o, int
 // Thread t always handles the channel quad 4 (t & 7) (ET is a multiple of 8), so its transform constants
 // are read from LDS once, into registers (reading them per element cost 2-way-conflicted LDS reads per
 // value); up to U float4 of x (and y) per thread are requested before the first transform.
-template <int PITCH>
+constexpr int SU = 8;  // float4 of x (and y) per thread per batch of stage_small
+// The first batch (base = threadIdx.x) of stage_small's loads, issued before the transform constants exist
+// (stage_small<PITCH, true> then starts from these registers): the kernel's prologue round trips overlap.
+// (Y: also the pre-BN tensor of a BN-backward operand)
+template <bool Y>
+__device__ __forceinline__ void small_prefetch(const Geo& g, const cv_operand& o, int n, int p0, int np, float4 (&v)[SU],
+                                               float4* yv) {
+  const int tot4 = np * (CS / 4);
+  const float4* x4 = reinterpret_cast<const float4*>(o.x + ((size_t)n * g.hs * g.ws + p0) * CS);
+  const float4* y4 = reinterpret_cast<const float4*>(o.y ? o.y + ((size_t)n * g.hs * g.ws + p0) * CS : nullptr);
+#pragma unroll
+  for (int q = 0; q < SU; ++q) {
+    const int i = threadIdx.x + q * ET;
+    v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (Y) yv[q] = v[q];
+    if (i < tot4) {
+      v[q] = x4[i];
+      if (Y) yv[q] = y4[i];
+    }
+  }
+}
+template <int PITCH, bool PRE = false>
 __device__ __forceinline__ void stage_small(const Geo& g, const cv_operand& o, int n, int p0, int np,
-                                            const BnFwdC* kf, const BnBwdC* kb, float* dst) {
-  constexpr int U = 8;
+                                            const BnFwdC* kf, const BnBwdC* kb, float* dst,
+                                            const float4* pv = nullptr, const float4* py = nullptr) {
+  constexpr int U = SU;
   const int tot4 = np * (CS / 4);
   const int c0 = (threadIdx.x & 7) * 4;
   BnFwdC f[4];
@@ -147,14 +188,22 @@ __device__ __forceinline__ void stage_small(const Geo& g, const cv_operand& o, i
   const float4* y4 = reinterpret_cast<const float4*>(o.y ? o.y + ((size_t)n * g.hs * g.ws + p0) * CS : nullptr);
   for (int base = threadIdx.x; base < tot4; base += ET * U) {
     float4 v[U], yv[U];
+    if (PRE && base == (int)threadIdx.x) {
 #pragma unroll
-    for (int q = 0; q < U; ++q) {
-      const int i = base + q * ET;
-      v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      yv[q] = v[q];
-      if (i < tot4) {
-        v[q] = x4[i];
-        if (o.xf == CV_XF_BNBWD) yv[q] = y4[i];
+      for (int q = 0; q < U; ++q) {
+        v[q] = pv[q];
+        yv[q] = py ? py[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int i = base + q * ET;
+        v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        yv[q] = v[q];
+        if (i < tot4) {
+          v[q] = x4[i];
+          if (o.xf == CV_XF_BNBWD) yv[q] = y4[i];
+        }
       }
     }
 #pragma unroll
@@ -213,7 +262,7 @@ __device__ __forceinline__ void stats_out(const float* s1, const float* s2, doub
 // 16-row tiles, lane l reads pixel 16i + (l&15) at tap-channel k = 4s + (l>>4).
 constexpr int GP = 36;  // LDS pitch (floats) of the gather's output tile
 template <int CB, int KK>
-__global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
+__global__ __launch_bounds__(ET, 3) void edge_gather_kernel(const EArgs P) {
   constexpr int NK = KK * KK * CB;
   constexpr int KS = (NK + 3) / 4;  // k-steps
   __shared__ BnFwdC kf[4];
@@ -245,6 +294,11 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
     const int tap = k / CB, c = k - tap * CB, kh = tap / KK, kw = tap - kh * KK;
     koff[st] = (k < NK) ? (kh * NC + kw) * CB + c : 0;
   }
+  // the band's first batch is requested before the constants (x-only operands: the register budget keeps
+  // 3 workgroups per CU; a BN-backward operand stages after them)
+  float bv[BU];
+  const bool pre = P.big.xf != CV_XF_BNBWD;
+  if (pre) big_load<CB, false>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, t, bv, nullptr);
   double* scratch = reinterpret_cast<double*>(sIn);  // (fold scratch: the staging area, unused yet)
   xf_consts(P.big, kf, kb, scratch);
   const int mode = P.ep.stat_mode;
@@ -256,7 +310,8 @@ __global__ __launch_bounds__(ET) void edge_gather_kernel(const EArgs P) {
     xf_consts(eo, ke, nullptr, scratch);
   }
   __syncthreads();
-  stage_big<CB>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kf, kb, sIn);
+  if (pre) stage_big<CB, true>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kf, kb, sIn, bv, nullptr);
+  else stage_big<CB>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kf, kb, sIn);
   __syncthreads();
   const int npx = R * g.ws;
   int abase[4];
@@ -428,12 +483,26 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   // [tap][cs][cb] (coalesced reads of the KK*KK*32*CB weights), pitch WKP: the 16 lanes of a b128 read hit
   // 16 disjoint 4-bank groups
   constexpr int WKP = 4 * CS + 4;
+  // the block-matrix weights: all 8 per thread in flight
   float* sWb = sIn + 4 * ET * 2;  // [16][WKP] behind the fold scratch, inside the (not yet used) staging area
-  for (int i = t; i < 16 * 4 * CS; i += ET) {
-    const int col = i / (4 * CS), k = i - col * (4 * CS), q = k / CS, ch = k - q * CS;
-    const int c2 = col / CB, c3 = col - c2 * CB;
-    const int kh = (c2 >> 1) + 2 - 2 * (q >> 1), kw = (c2 & 1) + 2 - 2 * (q & 1);
-    sWb[col * WKP + k] = (col < NCOL && kh < KK && kw < KK) ? P.w[((kh * KK + kw) * CS + ch) * CB + c3] : 0.f;
+  {
+    constexpr int NWB = 16 * 4 * CS / ET;
+    static_assert(NWB * ET == 16 * 4 * CS, "block matrix: whole rounds of ET");
+    float wv[NWB];
+#pragma unroll
+    for (int r = 0; r < NWB; ++r) {
+      const int i = t + r * ET;
+      const int col = i / (4 * CS), k = i - col * (4 * CS), q = k / CS, ch = k - q * CS;
+      const int c2 = col / CB, c3 = col - c2 * CB;
+      const int kh = (c2 >> 1) + 2 - 2 * (q >> 1), kw = (c2 & 1) + 2 - 2 * (q & 1);
+      wv[r] = (col < NCOL && kh < KK && kw < KK) ? P.w[((kh * KK + kw) * CS + ch) * CB + c3] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NWB; ++r) {
+      const int i = t + r * ET;
+      const int col = i / (4 * CS), k = i - col * (4 * CS);
+      sWb[col * WKP + k] = wv[r];
+    }
   }
   const int cls = nl / CB, cb = nl - cls * CB, cy = cls >> 1, cx = cls & 1;
   if (t < CB) sb[t] = P.bias ? P.bias[t] : 0.f;
@@ -450,7 +519,9 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
     }
   }
   __syncthreads();  // (the staging below overwrites the block matrix)
-  if (nrs > 0) stage_small<SP>(g, P.small, n, ys_lo * g.ws, nrs * g.ws, kf, kb, sIn);
+  if (nrs > 0) {
+    stage_small<SP>(g, P.small, n, ys_lo * g.ws, nrs * g.ws, kf, kb, sIn);
+  }
   __syncthreads();
   const float bias = nl < NCOL ? sb[cb] : 0.f;
   const int nblk = RBb * nbx, ntile = (nblk + 15) / 16;
@@ -721,7 +792,7 @@ __global__ __launch_bounds__(ET) void edge_wgrad_kernel(const EArgs P) {
 // edge_gather_kernel and edge_wgrad_kernel, so the outputs are bit-identical to the two separate launches.
 // P: the gather's arguments (big = gout, out = gin, ep), Q: the weight gradient's (small = X, out = partials).
 template <int CB, int KK, int NT>
-__global__ __launch_bounds__(ET) void edge_bwd_kernel(const EArgs P, const EArgs Q) {
+__global__ __launch_bounds__(ET, 2) void edge_bwd_kernel(const EArgs P, const EArgs Q) {
   constexpr int NK = KK * KK * CB;
   constexpr int KS = (NK + 3) / 4;
   __shared__ BnFwdC kfs[CS];  // the small side's forward constants (weight-gradient transform, epilogue mask)
