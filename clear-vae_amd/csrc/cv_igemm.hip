@@ -711,10 +711,25 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
     const int ncs = min(PK_CS, cs - cs0), ncb = min(PK_CB, cbn - cb0);
     const int run = ncb * kk;  // contiguous floats per cs row of the block
     const FDiv f_run = FDiv::make(run), f_kk = FDiv::make(kk), f_cs = FDiv::make(ncs), f_cb = FDiv::make(ncb);
-    for (int e = threadIdx.x; e < ncs * run; e += 256) {
-      const int i = f_run.div(e), r = e - i * run;  // r = (cb - cb0)*kk + tap
-      const int j = f_kk.div(r), tap = r - j * kk;
-      tile[(i * PK_CB + j) * pitch + tap] = src[((size_t)(cs0 + i) * cbn + cb0) * kk + r];
+    // PU loads per thread in flight (one round trip per PU * 256 elements; a load -> LDS store per
+    // iteration walked the 8K-element block in 32 dependent round trips)
+    constexpr int PU = 8;
+    const int tot = ncs * run;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += 256 * PU) {
+      float v[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int e = e0 + u * 256;
+        const int i = f_run.div(e), r = e - i * run;
+        v[u] = e < tot ? src[((size_t)(cs0 + i) * cbn + cb0) * kk + r] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int e = e0 + u * 256;
+        const int i = f_run.div(e), r = e - i * run;  // r = (cb - cb0)*kk + tap
+        const int j = f_kk.div(r), tap = r - j * kk;
+        if (e < tot) tile[(i * PK_CB + j) * pitch + tap] = v[u];
+      }
     }
     __syncthreads();
     if (a.dg[l])  // [tap][cb][cs]: runs of ncs

@@ -611,9 +611,17 @@ __global__ __launch_bounds__(256) void mi_learn_reduce_kernel(const LearnArgs A,
         const int a = j / S.inner[s], b = j - a * S.inner[s];
         off = S.poff[s] + (S.trans[s] ? b * 64 + a : a * 64 + b);
       }
-      // block order kept (deterministic), 8 partials in flight per batch instead of one load per add
+      // block order kept (deterministic), 32 partials in flight per batch (8 per batch left the 64-block
+      // fold 8 dependent round trips long)
       g = 0.f;
       int bl = 0;
+      for (; bl + 32 <= nb; bl += 32) {
+        float pv[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) pv[q] = W.gpart[(size_t)(bl + q) * MI_GSZ + off];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) g += pv[q];
+      }
       for (; bl + 8 <= nb; bl += 8) {
         float pv[8];
 #pragma unroll
@@ -642,7 +650,15 @@ __global__ __launch_bounds__(256) void mi_learn_reduce_kernel(const LearnArgs A,
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.loss_out) {
     double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += W.lpart[b];
+    int b = 0;
+    for (; b + 16 <= nb; b += 16) {  // (16 loads in flight, block order kept)
+      double lv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) lv[q] = W.lpart[b + q];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += lv[q];
+    }
+    for (; b < nb; ++b) s += W.lpart[b];
     A.loss_out[0] = (float)(-(s / (double)A.n));
   }
   if (!adam) return;
