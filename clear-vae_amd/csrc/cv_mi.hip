@@ -42,15 +42,35 @@ __device__ __forceinline__ void stage_mlp(const cv_mlp& P, MlpLds<DM>& L) {
   constexpr int PW = MlpLds<DM>::PW;
   const int t = threadIdx.x, nt = blockDim.x;
   const int dx = P.dx, h = P.h, dy = P.dy;
-  for (int i = t; i < h * dx; i += nt) {
-    const int u = i / dx, k = i - u * dx;
-    L.w1[u * PW + k] = P.w1[i];
-    L.w3[u * PW + k] = P.w3[i];
-  }
-  for (int i = t; i < dy * h; i += nt) {
-    const int k = i / h, u = i - k * h;
-    L.w2[k * PW + u] = P.w2[i];
-    L.w4[k * PW + u] = P.w4[i];
+  // SU elements of each matrix per thread in flight per round trip, the four matrices' loads issued
+  // together (a load -> LDS store per element made the staging one dependent round trip per element)
+  constexpr int SU = 4;
+  const int n13 = h * dx, n24 = dy * h;
+  const int nn = n13 > n24 ? n13 : n24;
+  for (int i0 = t; i0 < nn; i0 += nt * SU) {
+    float a1[SU], a3[SU], a2[SU], a4[SU];
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+      const int i = i0 + q * nt;
+      a1[q] = i < n13 ? P.w1[i] : 0.f;
+      a3[q] = i < n13 ? P.w3[i] : 0.f;
+      a2[q] = i < n24 ? P.w2[i] : 0.f;
+      a4[q] = i < n24 ? P.w4[i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+      const int i = i0 + q * nt;
+      if (i < n13) {
+        const int u = i / dx, k = i - u * dx;
+        L.w1[u * PW + k] = a1[q];
+        L.w3[u * PW + k] = a3[q];
+      }
+      if (i < n24) {
+        const int k = i / h, u = i - k * h;
+        L.w2[k * PW + u] = a2[q];
+        L.w4[k * PW + u] = a4[q];
+      }
+    }
   }
   for (int i = t; i < 64; i += nt) {
     L.b1[i] = (i < h) ? P.b1[i] : 0.f;
@@ -340,14 +360,39 @@ __global__ __launch_bounds__(256) void mi_rows_kernel(const MiArgs A) {
   }
   if (!last_block(W.ticket, &flag)) return;
   const int nb = gridDim.x;
+  // the workgroup partials folded in block order, FB blocks' loads in flight per batch (one dependent
+  // load per block made this last workgroup the launch's tail)
+  constexpr int FB = 16;
   if (t < 64) {
     double e = 0.0, m = 0.0;
-    for (int b = 0; b < nb; ++b) { e += W.fpart[b * MI_FP + 2 + t]; m += W.fpart[b * MI_FP + 66 + t]; }
+    int b = 0;
+    for (; b + FB <= nb; b += FB) {
+      double ev[FB], mv[FB];
+#pragma unroll
+      for (int q = 0; q < FB; ++q) {
+        ev[q] = W.fpart[(b + q) * MI_FP + 2 + t];
+        mv[q] = W.fpart[(b + q) * MI_FP + 66 + t];
+      }
+#pragma unroll
+      for (int q = 0; q < FB; ++q) { e += ev[q]; m += mv[q]; }
+    }
+    for (; b < nb; ++b) { e += W.fpart[b * MI_FP + 2 + t]; m += W.fpart[b * MI_FP + 66 + t]; }
     W.sums[128 + t] = e;
     W.sums[192 + t] = m;
   } else if (t == 64) {
     double a0 = 0.0, a1 = 0.0;
-    for (int b = 0; b < nb; ++b) { a0 += W.fpart[b * MI_FP]; a1 += W.fpart[b * MI_FP + 1]; }
+    int b = 0;
+    for (; b + FB <= nb; b += FB) {
+      double v0[FB], v1[FB];
+#pragma unroll
+      for (int q = 0; q < FB; ++q) {
+        v0[q] = W.fpart[(b + q) * MI_FP];
+        v1[q] = W.fpart[(b + q) * MI_FP + 1];
+      }
+#pragma unroll
+      for (int q = 0; q < FB; ++q) { a0 += v0[q]; a1 += v1[q]; }
+    }
+    for (; b < nb; ++b) { a0 += W.fpart[b * MI_FP]; a1 += W.fpart[b * MI_FP + 1]; }
     double mi;
     if (A.kind == CV_MI_CLUBSAMPLE) {
       mi = a0 / (double)n / 2.0;

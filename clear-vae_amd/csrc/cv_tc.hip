@@ -195,7 +195,15 @@ __global__ __launch_bounds__(256) void tc_learn_reduce_kernel(const TcArgs A, in
   const int Z = A.D.zdim, NP = TC_NP(Z);
   for (int e = blockIdx.x * 256 + threadIdx.x; e < NP; e += gridDim.x * 256) {
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += A.work[TC_MAXB + (size_t)b * NP + e];
+    int b = 0;
+    for (; b + 16 <= nb; b += 16) {  // (16 partials in flight, workgroup order kept)
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = A.work[TC_MAXB + (size_t)(b + q) * NP + e];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += v[q];
+    }
+    for (; b < nb; ++b) s += A.work[TC_MAXB + (size_t)b * NP + e];
     if (e < Z * Z) A.G.w1[e] = s;
     else if (e < Z * Z + Z) A.G.b1[e - Z * Z] = s;
     else if (e < Z * Z + 2 * Z) A.G.w2[e - Z * Z - Z] = s;
