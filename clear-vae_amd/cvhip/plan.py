@@ -739,6 +739,10 @@ class Workspace:
     # BatchNorm1d and ReLU in one launch, and the mask + BN1d backward + Linear weight gradient in one launch
     # (CVHIP_FUSED_DECIN=0: the separate reparam / Linear / bn_apply and mask / weight-gradient launches)
     FUSED_DECIN = os.environ.get("CVHIP_FUSED_DECIN", "1") != "0"
+    # CVHIP_DECIN_DRAW=1: the decoder-input launch draws z itself when the step has not (the CLEAR-MIM estimator
+    # forwards); every one of its workgroups then redraws all n x 2d latents.  Default: one cv_reparam_forward
+    # launch first (measured: 26.4 us for the drawing launch vs ~5 + 11.7 us)
+    DECIN_DRAW = os.environ.get("CVHIP_DECIN_DRAW", "0") == "1"
 
     def fused_decoder_input(self) -> bool:
         sp = self.spec
@@ -761,6 +765,11 @@ class Workspace:
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
         if self.fused_decoder_input():
+            if reparam is not None and not self.DECIN_DRAW:  # z drawn once, by its own launch
+                eps, seed, offset = reparam
+                P.add("cv_reparam_forward", self.heads, n, sp.d, eps.data_ptr() if eps is not None else None,
+                      ctypes.c_uint64(seed), offset.data_ptr() if offset is not None else None, z, None)
+                reparam = None
             eps, seed, offset = reparam if reparam is not None else (None, 0, None)
             P.add("cv_decoder_input_forward", lin, self.heads if reparam is not None else None,
                   eps.data_ptr() if eps is not None else None, ctypes.c_uint64(seed),

@@ -2,6 +2,7 @@
 shape is outside a fused kernel's contract) and at shapes outside the contracts, against the fp64 oracle with the
 bars of test_gpu_parity.py:
 
+  * Workspace.DECIN_DRAW = True: z drawn inside the decoder-input launch instead of by cv_reparam_forward;
   * Workspace.FUSED_DECIN / FUSED_HEADS / FUSED_HEADS_FWD / FUSED_EDGE_BWD = False: the separate reparameterisation,
     DENSE GEMMs, BN1d apply, mask / weight-gradient launches and the two edge backward launches;
   * n = 1100 (n x 2d > the decoder-input kernel's LDS budget, so the engine falls back on its own) and z = 12 / 20
@@ -22,16 +23,17 @@ pytestmark = pytest.mark.gpu
 KNOBS = ["FUSED_DECIN", "FUSED_HEADS", "FUSED_HEADS_FWD", "FUSED_EDGE_BWD"]
 
 
-def _run(n, zt, off, seed=5):
+def _run(n, zt, off, seed=5, draw=False):
     from oracle import cpu_ref as R
     from cvhip import rng
     from cvhip.engine import ClearStep
     from cvhip.plan import Workspace
 
-    saved = {k: getattr(Workspace, k) for k in KNOBS}
+    saved = {k: getattr(Workspace, k) for k in KNOBS + ["DECIN_DRAW"]}
     try:
         for k in off:
             setattr(Workspace, k, False)
+        Workspace.DECIN_DRAW = draw
         arch, C = "VAE", 1
         sd = R.det_state(arch, zt, C)
         x, label, ec, es, _ = R.det_inputs(n, C, 28, zt, 10, seed=seed)
@@ -60,6 +62,12 @@ def _run(n, zt, off, seed=5):
                          ids=lambda v: "+".join(v))
 def test_unfused_paths_match_oracle(off):
     _run(64, 16, off)
+
+
+def test_decoder_input_drawing_z_matches_oracle():
+    """Heads forward unfused, so z is drawn by the decoder-input launch itself (Workspace.DECIN_DRAW; the default
+    draws it with one cv_reparam_forward launch first)."""
+    _run(64, 16, ["FUSED_HEADS_FWD"], draw=True)
 
 
 @pytest.mark.parametrize("n,zt", [(1100, 16), (64, 12), (64, 20)])
