@@ -426,10 +426,12 @@ class ClearStep:
             # so they are computed once; each update re-runs the reparameterisation (fresh noise), the decoder
             # (its statistics follow z) and the running-statistics update of every layer (the encoder's five
             # momentum updates with its one set of batch statistics, as in five forwards)
+            # (the statistics of the first estimator forward are zeroed by the pack launch before it)
+            stats_zero = [(ws.stats, ws.stats.numel() * 8)]
+
             def learn_forward(prog, j, inject):
                 rp = (eps_buf[1 + j] if inject else None, self.seed, self.offset)
                 if j == 0:
-                    prog.add("cv_zero", ws.stats, ws.stats.numel() * 8)
                     if ws.encoder_program(prog, X, True, reparam=rp):
                         return None  # (z drawn by the heads launch)
                 else:
@@ -439,7 +441,7 @@ class ClearStep:
 
             def make_learn(inject: bool):
                 lp = Program()
-                pack_program(sp, lp, "all")  # the VAE Adam step just moved the weights
+                pack_program(sp, lp, "all", zero=stats_zero)  # the VAE Adam step just moved the weights
                 for j in range(5):
                     ws.decoder_program(lp, ws.z, True, "none", reparam=learn_forward(lp, j, inject))
                     ws.running_program(lp, "all")
@@ -455,7 +457,7 @@ class ClearStep:
                 for j in range(5):
                     gp = Program()
                     if j == 0:
-                        pack_program(sp, gp, "all")
+                        pack_program(sp, gp, "all", zero=stats_zero)
                     ws.decoder_program(gp, ws.z, True, "none", reparam=learn_forward(gp, j, inject))
                     ws.running_program(gp, "all")
                     gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
@@ -479,8 +481,8 @@ class ClearStep:
                 # trainer.py:680-699: a second train-mode forward (fresh noise) on the updated VAE, then the
                 # discriminator's BCE gradients and its Adam step (data parallel: all-reduce in between)
                 gp = Program()
-                pack_program(sp, gp, "all")  # the VAE Adam step just moved the weights
-                gp.add("cv_zero", ws.stats, ws.stats.numel() * 8)
+                # the VAE Adam step just moved the weights; the same launch zeroes the forward's statistics
+                pack_program(sp, gp, "all", zero=[(ws.stats, ws.stats.numel() * 8)])
                 rp = (eps_buf[1] if inject else None, self.seed, self.offset)
                 drew = ws.encoder_program(gp, X, True, reparam=rp)
                 ws.decoder_program(gp, ws.z, True, "none", reparam=None if drew else rp)
