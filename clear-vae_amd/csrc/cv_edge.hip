@@ -697,7 +697,7 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
 // column offsets.  The waves' 32 x ncol partials are folded in LDS in wave order.
 constexpr int WP = 48;
 template <int CB, int KK, int NT>
-__global__ __launch_bounds__(ET) void edge_wgrad_kernel(const EArgs P) {
+__global__ __launch_bounds__(ET, 3) void edge_wgrad_kernel(const EArgs P) {
   constexpr int NK = KK * KK * CB;
   __shared__ BnFwdC kfs[CS];
   __shared__ BnBwdC kbs[CS];
@@ -709,11 +709,18 @@ __global__ __launch_bounds__(ET) void edge_wgrad_kernel(const EArgs P) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int kq = lane >> 4, nl = lane & 15;
   const int ncol = P.ncol;
+  const int R = P.rows;
+  const int NC = (g.ws - 1) * g.s + KK;
+  // the big band's first batch (x-only operands, e.g. the input image) is requested before the constants
+  const int nbk = (g.hs + R - 1) / R;
+  const int n0 = blockIdx.x / nbk, r00 = (blockIdx.x - n0 * nbk) * R;
+  const int NR0 = (min(R, g.hs - r00) - 1) * g.s + KK;
+  float bv[BU];
+  const bool pre = P.big.xf != CV_XF_BNBWD;
+  if (pre) big_load<CB, false>(g, P.big, n0, r00 * g.s - g.p, -g.p, NR0, NC, t, bv, nullptr);
   xf_consts(P.small, kfs, kbs, scratch);
   xf_consts(P.big, kfb, kbb, scratch);
   __syncthreads();
-  const int R = P.rows;
-  const int NC = (g.ws - 1) * g.s + KK;
   float* sA = lds;                          // [R*ws][WP]
   float* sB = lds + (size_t)R * g.ws * WP;  // [NR][NC][CB] (+1 zero word)
   // this lane's columns: offset in a receptive field, or -1 (bias: ones), -2 (padding: zeros)
@@ -742,7 +749,8 @@ __global__ __launch_bounds__(ET) void edge_wgrad_kernel(const EArgs P) {
       const int Rb = min(R, g.hs - r0);
       const int NR = (Rb - 1) * g.s + KK;
       stage_small<WP>(g, P.small, n, r0 * g.ws, Rb * g.ws, kfs, kbs, sA);
-      stage_big<CB>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kfb, kbb, sB);
+      if (pre) stage_big<CB, true>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kfb, kbb, sB, bv, nullptr);
+      else stage_big<CB>(g, P.big, n, r0 * g.s - g.p, -g.p, NR, NC, kfb, kbb, sB);
       __syncthreads();
       const int npx = Rb * g.ws;
       for (int p0 = 4 * w; p0 < npx; p0 += 16) {
