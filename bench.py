@@ -750,6 +750,17 @@ def main():
                     rec["cpu_baseline"] = cpu_baseline(cfg)
                 except Exception as e:  # pragma: no cover
                     rec["cpu_baseline"] = {"error": repr(e)}
+                if args.config == "mnist" and args.batch is None:
+                    # BASELINE configs[0]: Styled-MNIST bs=64 CLEAR-VAE on the reference's CPU path
+                    # (reference step: code/src/trainer.py:435-493), timed on the same host cores
+                    try:
+                        c1 = list(cfg)
+                        c1[4] = 64
+                        rec["cpu_baseline_c1"] = dict(cpu_baseline(tuple(c1), budget_s=8.0),
+                                                      config="configs[0]: Styled-MNIST 28x28 bs=64 CLEAR-VAE, "
+                                                             "reference CPU path (no GPU)")
+                    except Exception as e:  # pragma: no cover
+                        rec["cpu_baseline_c1"] = {"error": repr(e)}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

@@ -1004,16 +1004,22 @@ __global__ __launch_bounds__(ET, 2) void edge_bwd_kernel(const EArgs P, const EA
 
 // ---------------------------------------------------------------- host side
 // small-grid rows per band of the gather / weight-gradient / fused backward launches: one row per thread
-// (ET / ws), at most the image; CV_EDGE_ROWS=<rows> overrides (A/B knob)
+// (ET / ws), at most the image; CV_EDGE_ROWS=<rows> overrides (A/B knob), clamped to ET / ws: the gather and
+// fused-backward kernels compute ET pixels per band (one per thread), so a taller band would leave its
+// last pixels unwritten in the LDS output tile that the epilogue streams out
+int edge_rows_for(int ws, int hs, int ovr) {
+  const int cap = ws >= ET ? 1 : ET / ws;
+  int r = cap;
+  if (ovr > 0) r = ovr < cap ? ovr : cap;
+  return r > hs ? hs : r;
+}
 static int edge_rows(const Geo& g) {
   static int ovr = -2;
   if (ovr == -2) {
     const char* e = getenv("CV_EDGE_ROWS");
     ovr = e ? atoi(e) : -1;
   }
-  int r = g.ws >= ET ? 1 : ET / g.ws;
-  if (ovr > 0) r = ovr;
-  return r > g.hs ? g.hs : r;
+  return edge_rows_for(g.ws, g.hs, ovr);
 }
 
 static bool ep_ok(const cv_epilogue* ep, int C) {

@@ -548,7 +548,7 @@ class ClearStep:
                 seg += [("prog", [gp]), ("ar_est",), ("wait_est",), ("prog", [ap])]
         return seg
 
-    def _run_segments(self, segs, graphs=None):
+    def _run_segments(self, segs, graphs=None, upd=None, before_update=None):
         s = _lib.stream_handle()
         gi = 0
         for item in segs:
@@ -556,6 +556,8 @@ class ClearStep:
             if kind == "prog":
                 if graphs is None:
                     for P in item[1]:
+                        if before_update is not None and P is upd:
+                            before_update()
                         P.run(s)
                 else:
                     graphs[gi].replay()
@@ -583,8 +585,8 @@ class ClearStep:
         e1.record()
         self.comm_probe.append(("vae" if buckets is self.buckets else "est", e0, e1))
 
-    def _run_eager(self, G, inject=False):
-        self._run_segments(self._segments(G, inject))
+    def _run_eager(self, G, inject=False, before_update=None):
+        self._run_segments(self._segments(G, inject), upd=G["upd"], before_update=before_update)
 
     def _take_injections(self, G) -> bool:
         """Consume queued test noise (cvhip.rng): eps_c, eps_s for the main forward and, in CLEAR-MIM,
@@ -634,7 +636,11 @@ class ClearStep:
             G["X"].copy_(X, non_blocking=True)
             G["lab"].copy_(lab, non_blocking=True)
 
-    def step(self, X, label):
+    def step(self, X, label, before_update=None):
+        """One training step on the batch (X, label).  before_update: an optional callable run (on the host, in
+        stream order: the step's kernels before it are enqueued, none after) once the gradients are complete —
+        all-reduced under DP — and before the Adam launch; such a step runs eagerly, not from the graph (used by
+        the tests to read the step's activations with the pre-update parameters)."""
         n = X.shape[0]
         G = self.graphs.get(n)
         if G is None:
@@ -646,13 +652,13 @@ class ClearStep:
             self.est_adam.refresh_hyper()
         self._load_batch(G, X, label)
         inject = self._take_injections(G)
-        use_graph = G["count"] >= 1 and not inject and self.graphs_enabled
+        use_graph = G["count"] >= 1 and not inject and self.graphs_enabled and before_update is None
         if use_graph and "graphs" not in G:
             self._capture(G)
         if use_graph:
             self._run_segments(self._segments(G, False), G["graphs"])
         else:
-            self._run_eager(G, inject)
+            self._run_eager(G, inject, before_update)
         G["count"] += 1
         self.steps_since_sync += 1
         self.anneal_expected += 1

@@ -260,7 +260,7 @@ def set_precision(vae: nn.Module, precision: str = "fp32"):
     """Operand precision of the model's conv / linear contractions on the HIP path: "fp32" (the
     reference's arithmetic, default) or "bf16" (BASELINE configs[4]: operands rounded to bf16 for
     v_mfma_f32_16x16x32_bf16, fp32 accumulation; activations, BatchNorm statistics, losses and Adam stay
-    fp32).  Takes effect at the next step: a fused engine built for the other precision rebuilds."""
+    fp32, as do the image-facing first conv / last convT and the latent-side linears, LIN_MMA).  Takes effect at the next step: a fused engine built for the other precision rebuilds."""
     if precision not in _lib.PRECISION:
         raise ValueError(f"precision must be one of {sorted(_lib.PRECISION)}, got {precision!r}")
     vae._cv_precision = precision
@@ -404,6 +404,14 @@ _SIDE_STREAMS: dict = {}
 # or faster on both bench configs (MNIST 0.7015 vs 0.7046 ms, CelebA-MIM 6.46 vs 6.60 ms).
 # CVHIP_SIDE_STREAM=1 restores the two-stream schedule.
 SIDE_STREAM = os.environ.get("CVHIP_SIDE_STREAM", "0") == "1"
+
+# Operand precision of the latent-side linear layers (the four heads and the decoder Linear) under either model
+# precision: fp32.  Their fused kernels (cv_declinear.hip: cv_heads_forward / _backward,
+# cv_decoder_input_forward / _backward) run v_mfma_f32_16x16x4_f32 only, and they are < 0.4 % of a VAE64 step's
+# FLOPs, so precision="bf16" applies to the conv / convT contractions of the GEMM core alone; the DENSE fallback
+# (batches the fused kernels do not serve) is given the same fp32 geometry so the arithmetic does not depend on
+# the batch size.  oracle/cpu_ref.py `bf16=` restates exactly this split.
+LIN_MMA = _lib.MMA_FP32
 
 
 def _side_stream(device) -> "torch.cuda.Stream":
@@ -709,7 +717,7 @@ class Workspace:
             cur = self.y_enc[li]
         # heads (Linear on the NCHW-flattened activation)
         C, Hh, Wh = sp.feat
-        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
+        lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, LIN_MMA)
         if self.fused_heads_forward():
             eps, seed, offset = reparam if reparam is not None else (None, 0, None)
             P.add("cv_heads_forward", lin, cur, self.bn_enc[-1].cv(train), sp.heads_wp, sp.heads[0].bias.data_ptr(),
@@ -763,7 +771,7 @@ class Workspace:
         fused decoder-input launch); None: z is given."""
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
-        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
+        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
         if self.fused_decoder_input():
             if reparam is not None and not self.DECIN_DRAW:  # z drawn once, by its own launch
                 eps, seed, offset = reparam
@@ -818,7 +826,7 @@ class Workspace:
                 xin = operand(self.ah)
             self._wgrad_call(P, "conv", g, xin, gout, param_grad(c.mod.weight), None, ("dec", li), defer)
         Cu, Hu, Wu = sp.unflat
-        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, sp.mma)
+        lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
         if self.fused_decoder_input():  # gah <- d(h) in place, weight gradient, BN1d backward sums, dz
             if zero_dz:
                 P.add("cv_zero", dz_out, dz_out.numel() * 4)
@@ -841,11 +849,11 @@ class Workspace:
         sp, n = self.spec, self.n
         C, Hh, Wh = sp.feat
         if heads and self.fused_heads():
-            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
+            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, LIN_MMA)
             P.add("cv_heads_backward", lin, dheads, sp.heads[0].weight, self.y_enc[-1], self.bn_enc[-1].cv(True),
                   self.g_enc[-1], self.bn_enc[-1].gstat, param_grad(sp.heads[0].weight), param_grad(sp.heads[0].bias))
         elif heads:
-            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, sp.mma)
+            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, LIN_MMA)
             a_last = operand(self.y_enc[-1], XF_BNRELU, self.bn_enc[-1].cv(True))
             self._wgrad_call(P, "linear", lin, operand(dheads), a_last, param_grad(sp.heads[0].weight),
                              param_grad(sp.heads[0].bias), ("heads",), defer)

@@ -519,7 +519,12 @@ int cv_debug_force_generic_gemm(int on);
 /* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
  * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least
  * cv_gemm_workspace_bytes(), ZEROED before registration, for the current device (NULL: unregister).
- * Calls on one stream share it; without one the launches run unsplit.  No reference counterpart
+ * Calls on one stream share it; without one the launches run unsplit.  CONTRACT: the split launches of a
+ * device must be serialised — one stream at a time (the fused step engine issues them all on its step
+ * stream; the autograd path on torch's current stream).  Two split launches in flight on different streams
+ * would race on its fragment slabs and leave its self-resetting per-tile tickets non-zero, corrupting every
+ * later split launch; a caller that runs conv layers on several streams concurrently registers NULL (no
+ * split) or serialises them with events.  No reference counterpart
  * (the reference's convolutions are ATen's, code/src/models/vae.py:15-46 / :113-156). */
 size_t cv_gemm_workspace_bytes(void);
 int cv_set_gemm_workspace(void* work, size_t bytes);

@@ -195,28 +195,77 @@ def _relu(h, masks, key):
     return F.relu(h)
 
 
-def encode(P, x, arch, train=True, masks=None):
-    """vae.py:48-50 (encoder 15-26 / 113-130, heads 27-30); masks: _relu."""
+def _r16(t):
+    """Round to bf16 (nearest even) and back: an operand as the bf16 MFMA path stages it."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    """conv2d / conv_transpose2d with the contraction operands rounded to bf16 where the HIP GEMM core rounds
+    them under precision="bf16" (cv_gemm_tile.inc `store`: after the fp32 BN transform, before the LDS image):
+    forward the input activation and the weight; backward the incoming gradient (after the BN backward) in
+    both the data and the weight contraction, together with the weight resp. the input activation.  The
+    contraction itself stays exact here (fp64 or fp32 accumulation).  Bias gradient: the unrounded sum."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, s, p, op, transposed):
+        hr, wr = _r16(h), _r16(w)
+        ctx.save_for_backward(hr, wr)
+        ctx.cfg = (s, p, op, transposed, b is not None)
+        return _Bf16Conv._conv(hr, wr, s, p, op, transposed) + (0 if b is None else b.view(1, -1, 1, 1))
+
+    @staticmethod
+    def _conv(h, w, s, p, op, transposed):
+        if transposed:
+            return F.conv_transpose2d(h, w, None, stride=s, padding=p, output_padding=op)
+        return F.conv2d(h, w, None, stride=s, padding=p)
+
+    @staticmethod
+    def backward(ctx, g):
+        hr, wr = ctx.saved_tensors
+        s, p, op, transposed, has_b = ctx.cfg
+        with torch.enable_grad():
+            h_, w_ = hr.detach().requires_grad_(True), wr.detach().requires_grad_(True)
+            out = _Bf16Conv._conv(h_, w_, s, p, op, transposed)
+            gh, gw = torch.autograd.grad(out, (h_, w_), _r16(g))
+        gb = g.sum(dim=(0, 2, 3)) if has_b else None
+        return gh, gw, gb, None, None, None, None
+
+
+def _conv(h, P, name, s, p, op=0, transposed=False, bf16=False):
+    """One conv / convT layer; bf16: the GEMM-core operand rounding (_Bf16Conv)."""
+    w, b = P[f"{name}.weight"], P[f"{name}.bias"]
+    if bf16:
+        return _Bf16Conv.apply(h, w, b, s, p, op, transposed)
+    if transposed:
+        return F.conv_transpose2d(h, w, b, stride=s, padding=p, output_padding=op)
+    return F.conv2d(h, w, b, stride=s, padding=p)
+
+
+def encode(P, x, arch, train=True, masks=None, bf16=False):
+    """vae.py:48-50 (encoder 15-26 / 113-130, heads 27-30); masks: _relu.  bf16: the HIP path's precision="bf16"
+    arithmetic — every conv but the image-facing first one (an edge kernel, fp32 by design) takes bf16-rounded
+    operands (_Bf16Conv); the heads stay fp32 (cvhip/plan.py runs the latent-side linears in fp32)."""
     h = x
     i = 0
-    for cin, cout, k, s, p in ENC[arch]:
-        h = F.conv2d(h, P[f"encoder.{i}.weight"], P[f"encoder.{i}.bias"], stride=s, padding=p)
+    for j, (cin, cout, k, s, p) in enumerate(ENC[arch]):
+        h = _conv(h, P, f"encoder.{i}", s, p, bf16=bf16 and j > 0)
         h = _relu(_bn(h, P, f"encoder.{i + 1}", train), masks, f"encoder.{i + 2}")
         i += 3
     h = h.flatten(1)
     return tuple(F.linear(h, P[f"{n}.weight"], P[f"{n}.bias"]) for n in ("mu_c", "logvar_c", "mu_s", "logvar_s"))
 
 
-def decode(P, z, arch, train=True, masks=None):
-    """vae.py:52-54 (decoder 32-46 / 136-156); masks: _relu."""
+def decode(P, z, arch, train=True, masks=None, bf16=False):
+    """vae.py:52-54 (decoder 32-46 / 136-156); masks: _relu; bf16: as in encode (every ConvTranspose2d but the
+    image-facing last one; the decoder Linear stays fp32)."""
     h = F.linear(z, P["decoder.0.weight"], P["decoder.0.bias"])
     h = _relu(_bn(h, P, "decoder.1", train), masks, "decoder.2")
     h = h.unflatten(1, UNFLAT[arch])
     i = 4
     n_dec = len(DEC[arch])
     for j, (cin, cout, k, s, p, op) in enumerate(DEC[arch]):
-        h = F.conv_transpose2d(h, P[f"decoder.{i}.weight"], P[f"decoder.{i}.bias"], stride=s, padding=p,
-                               output_padding=op)
+        h = _conv(h, P, f"decoder.{i}", s, p, op, True, bf16=bf16 and j < n_dec - 1)
         h = _bn(h, P, f"decoder.{i + 1}", train)
         h = torch.sigmoid(h) if j == n_dec - 1 else _relu(h, masks, f"decoder.{i + 2}")
         i += 3
@@ -228,10 +277,10 @@ def sample(mu, logvar, eps):
     return mu + eps * torch.exp(0.5 * logvar)
 
 
-def vae_forward(P, x, eps_c, eps_s, arch, train=True, masks=None):
-    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, train, masks)
+def vae_forward(P, x, eps_c, eps_s, arch, train=True, masks=None, bf16=False):
+    mu_c, lv_c, mu_s, lv_s = encode(P, x, arch, train, masks, bf16)
     z = torch.cat([sample(mu_c, lv_c, eps_c), sample(mu_s, lv_s, eps_s)], dim=-1)
-    return decode(P, z, arch, train, masks), {"mu_c": mu_c, "logvar_c": lv_c, "mu_s": mu_s, "logvar_s": lv_s}, z
+    return decode(P, z, arch, train, masks, bf16), {"mu_c": mu_c, "logvar_c": lv_c, "mu_s": mu_s, "logvar_s": lv_s}, z
 
 
 # ----------------------------------------------------------------------------- losses
@@ -339,9 +388,10 @@ def anneal_weight(step, beta, loc=0, scale=1):
 # ----------------------------------------------------------------------------- one training step
 
 
-def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0, masks=None):
-    """One CLEARVAETrainer step's losses and gradients (trainer.py:452-482), no optimizer update."""
-    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks)
+def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0, masks=None, bf16=False):
+    """One CLEARVAETrainer step's losses and gradients (trainer.py:452-482), no optimizer update.  masks / bf16:
+    encode / decode (test-side pinning of the device's ReLU activity and of its bf16 operand rounding)."""
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks, bf16)
     rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
     c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
     s = contrastive_loss(lp["mu_s"], lp["logvar_s"], label, sim_fn, hp["temperature"], ps=hp["ps"])
@@ -358,9 +408,9 @@ def clear_step(P, x, label, eps_c, eps_s, arch, hp, sim_fn="cosine", step=0, mas
 
 
 def mim_step(P, M, x, label, eps_c, eps_s, perm, arch, hp, kind="CLUBSample", sim_fn="cosine", step=0,
-             masks=None):
+             masks=None, bf16=False):
     """The VAE half of one ClearMIMVAETrainer step (trainer.py:848-869): losses and VAE grads."""
-    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks)
+    xhat, lp, z = vae_forward(P, x, eps_c, eps_s, arch, True, masks, bf16)
     rec, kl_c, kl_s = vae_loss(xhat, x, lp["mu_c"], lp["mu_s"], lp["logvar_c"], lp["logvar_s"])
     c = contrastive_loss(lp["mu_c"], lp["logvar_c"], label, sim_fn, hp["temperature"])
     d = z.shape[1] // 2

@@ -11,7 +11,7 @@ import sys
 import traceback
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "clear-vae_amd"), ROOT):
+for p in (os.path.join(ROOT, "clear-vae_amd"), ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -107,8 +107,18 @@ def run(rank, world, port, q, mode, n_global, kind, arch="VAE", precision="fp32"
             out["perm"] = lperm
         X = torch.tensor(x[lo:hi], dtype=torch.float32, device=dev)
         L = torch.tensor(label[lo:hi], device=dev)
-        res = eng.step(X, L)
+        held = {}
+
+        def read_masks():  # the ReLU activity of this rank's shard, with the pre-Adam BN affine (tests/maskpin.py)
+            from maskpin import device_masks
+
+            held["m"] = device_masks(eng, eng.last_workspace(n), n)
+
+        res = eng.step(X, L, before_update=read_masks)
         torch.cuda.synchronize()
+        from maskpin import masks_to_numpy
+
+        out["masks"] = masks_to_numpy(held["m"])
         if mode in ("clear", "group"):
             out["losses"] = _np(res)
         else:

@@ -107,3 +107,19 @@ def test_struct_layouts_match_header(tmp_path):
             assert ctypes.sizeof(T) == int(parts[2]), line
         else:
             assert getattr(T, parts[1]).offset == int(parts[2]), line
+
+
+def test_host_validation_under_asan():
+    """`make asan` (SURVEY.md §5 host-side sanitizer build): the library's host code compiled host-only with
+    -fsanitize=address, and tests/abi_asan.c driving the C-ABI's validation paths and host-side builders
+    against it (no GPU: every call is rejected or answered before a launch).  A failed check or any ASan report
+    fails the run."""
+    csrc = os.path.join(ROOT, "clear-vae_amd", "csrc")
+    r = subprocess.run(["make", "-C", csrc, "asan", "-j8"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    exe = os.path.join(ROOT, "build", "asan", "abi_asan")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=23")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    assert "AddressSanitizer" not in r.stderr
+    assert "all host validation checks passed" in r.stdout

@@ -24,6 +24,7 @@ import pytest
 import torch
 
 import golden_cases as G
+from maskpin import device_masks
 from test_gpu_golden import _bias_before_bn, build_fused
 
 pytestmark = pytest.mark.gpu
@@ -36,30 +37,6 @@ pytestmark = pytest.mark.gpu
 MEDIAN_TOL = 5e-6
 WORST_TOL = 1e-5
 FLOOR_X = 8.0
-
-
-def device_masks(eng, ws, n):
-    from cvhip import _lib
-
-    sp = eng.spec
-    s = _lib.stream_handle()
-    masks = {}
-    for li, c in enumerate(sp.enc):
-        y = ws.y_enc[li]
-        out = torch.empty_like(y)
-        _lib.call("cv_bn_apply", ws.bn_enc[li].cv(True), y.data_ptr(), out.data_ptr(), n * c.h_out * c.w_out,
-                  c.c_out, 1, c.c_out, 0, s)
-        masks[f"encoder.{3 * li + 2}"] = (out > 0).view(n, c.h_out, c.w_out, c.c_out).permute(0, 3, 1, 2)
-    Cu, Hu, Wu = sp.unflat
-    masks["decoder.2"] = (ws.ah > 0).view(n, Hu * Wu, Cu).permute(0, 2, 1).reshape(n, Cu * Hu * Wu)
-    for li, c in enumerate(sp.dec[:-1]):
-        y = ws.y_dec[li]
-        out = torch.empty_like(y)
-        _lib.call("cv_bn_apply", ws.bn_dec[li].cv(True), y.data_ptr(), out.data_ptr(), n * c.h_out * c.w_out,
-                  c.c_out, 1, c.c_out, 0, s)
-        masks[f"decoder.{4 + 3 * li + 2}"] = (out > 0).view(n, c.h_out, c.w_out, c.c_out).permute(0, 3, 1, 2)
-    torch.cuda.synchronize()
-    return {k: v.double().cpu() for k, v in masks.items()}
 
 
 def oracle_grads(fx, masks, dtype=torch.float64):

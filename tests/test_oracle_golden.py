@@ -93,3 +93,39 @@ def test_clear_tc_factor_step(case):
         assert G.rel(g, fx["disc_grad__" + k]) < 1e-6, (name, k)
     for k, v in o["disc_after"].items():
         assert G.rel(v, fx["disc_after__" + k]) < 1e-9, (name, k)
+
+
+def test_bf16_conv_restatement():
+    """oracle/cpu_ref.py _Bf16Conv (the bf16 GEMM-core arithmetic the bf16 tests pin against): with operands
+    and incoming gradient already bf16-representable it is the plain fp64 conv / convT with its exact autograd;
+    otherwise it differs by bf16 rounding of exactly those three tensors."""
+    import torch.nn.functional as F
+
+    from oracle import cpu_ref as R
+
+    g = torch.Generator().manual_seed(0)
+    for transposed in (False, True):
+        h = torch.randn(2, 8, 6, 6, generator=g, dtype=torch.float64)
+        w = torch.randn(8, 4, 3, 3, generator=g, dtype=torch.float64) if transposed else \
+            torch.randn(4, 8, 3, 3, generator=g, dtype=torch.float64)
+        b = torch.randn(4, generator=g, dtype=torch.float64)
+        op = 1 if transposed else 0
+        for exact in (True, False):
+            hh, ww = (R._r16(h), R._r16(w)) if exact else (h, w)
+            a1, w1, b1 = (t.clone().requires_grad_(True) for t in (hh, ww, b))
+            y = R._Bf16Conv.apply(a1, w1, b1, 2, 1, op, transposed)
+            gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+            gy = R._r16(gy) if exact else gy
+            y.backward(gy)
+            a2, w2, b2 = (t.clone().requires_grad_(True) for t in (R._r16(hh), R._r16(ww), b))
+            f = (lambda u, v, c: F.conv_transpose2d(u, v, c, stride=2, padding=1, output_padding=1)) if transposed \
+                else (lambda u, v, c: F.conv2d(u, v, c, stride=2, padding=1))
+            y2 = f(a2, w2, b2)
+            y2.backward(R._r16(gy))
+            assert torch.allclose(y, y2, rtol=1e-12, atol=1e-12)
+            assert torch.allclose(a1.grad, a2.grad, rtol=1e-12, atol=1e-12)
+            assert torch.allclose(w1.grad, w2.grad, rtol=1e-12, atol=1e-12)
+            assert torch.allclose(b1.grad, gy.sum(dim=(0, 2, 3)))
+            if not exact:  # the rounding is really in effect
+                y3 = f(h, w, b)
+                assert float((y3 - y).abs().max()) > 1e-4
