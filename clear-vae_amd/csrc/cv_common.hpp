@@ -83,6 +83,12 @@ int edge_scatter_out(const Geo& g, const cv_operand* in, const float* ws, const 
 int edge_bwd(const Geo& g, const cv_operand* gout, const float* wg, float* gin, const cv_epilogue* ep,
              const cv_operand* x, float* gw, float* work, size_t work_bytes, hipStream_t st);
 
+// class-fused direct SCATTER (cv_direct.hip): stride-2 Conv2d backward-data / ConvTranspose2d forward with the
+// small-grid operand staged in LDS once per workgroup; wk = the k-contiguous packing [tap][cb][cs]; -1 when the
+// call is not one it serves
+int direct_scatter(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,
+                   const cv_epilogue* ep, hipStream_t st, int mma);
+
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1127,12 +1127,17 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
   return launch(a, BM_, BN_, 1, st);
 }
 
+// the k-contiguous packing [tap][cb][cs] of the current call's weights (cv_conv_*_kpack), else null
+static thread_local const float* g_wk = nullptr;
+
 // SCATTER with big = rows. `in` is the small-grid tensor; w is packed [tap][cs][cb].
 static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
                        const cv_epilogue* ep, hipStream_t st, const char* what, int mma) {
   if (!g_force_generic) {
     const int er = edge_scatter(g, in, w, bias, out, ep, st);
     if (er >= 0) return er;
+    const int dr = direct_scatter(g, in, g_wk, bias, out, ep, st, mma);
+    if (dr >= 0) return dr;
   }
   const int nr = narrow_scatter(g, in, w, bias, out, ep, st);
   if (nr >= 0) return nr;
@@ -1427,6 +1432,24 @@ extern "C" int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, c
   if (!g->transposed)
     return run_scatter(geo, gout, wpacked, nullptr, gin, ep, S(stream), "conv_backward_data", g->mma);
   return run_gather(geo, gout, wpacked, nullptr, gin, ep, S(stream), "convT_backward_data", g->mma);
+}
+
+extern "C" int cv_conv_forward_kpack(const cv_conv* g, const cv_operand* in, const float* wpacked,
+                                     const float* wkpack, const float* bias, float* out, const cv_epilogue* ep,
+                                     cv_stream_t stream) {
+  g_wk = wkpack;
+  const int r = cv_conv_forward(g, in, wpacked, bias, out, ep, stream);
+  g_wk = nullptr;
+  return r;
+}
+
+extern "C" int cv_conv_backward_data_kpack(const cv_conv* g, const cv_operand* gout, const float* wpacked,
+                                           const float* wkpack, float* gin, const cv_epilogue* ep,
+                                           cv_stream_t stream) {
+  g_wk = wkpack;
+  const int r = cv_conv_backward_data(g, gout, wpacked, gin, ep, stream);
+  g_wk = nullptr;
+  return r;
 }
 
 extern "C" size_t cv_conv_wgrad_workspace_bytes(const cv_conv* g, int split_k) {

@@ -154,6 +154,10 @@ _SIGS = {
     "cv_pack_conv_weights_zero": (c_int, [_P(cv_conv_pack), c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "cv_conv_forward": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_data": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
+    "cv_conv_forward_kpack": (
+        c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
+    "cv_conv_backward_data_kpack": (
+        c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),
     "cv_conv_backward_weight": (
         c_int,
         [_P(cv_conv), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p],
@@ -328,6 +332,7 @@ _SIGS = {
     "cv_last_error": (ctypes.c_char_p, []),
     "cv_version": (c_int, []),
     "cv_debug_force_generic_gemm": (c_int, [c_int]),
+    "cv_debug_direct_count": (c_int, [c_int]),
     "cv_gemm_workspace_bytes": (c_size_t, []),
     "cv_set_gemm_workspace": (c_int, [c_void_p, c_size_t]),
 }

@@ -56,6 +56,7 @@ class ConvSpec:
     # GEMM-native weight copies (cv_pack_conv_weights): read by the forward / backward-data launch
     wfwd: object = None
     wbwd: object = None
+    wk: object = None  # the `gather` packing Wg[tap][cb][cs]: the k-contiguous B image of the SCATTER contraction
     mma: int = 0  # CV_MMA_* operand precision of this layer's GEMMs (cvhip.set_precision)
 
     def geom(self, n: int) -> cv_conv:
@@ -287,6 +288,7 @@ def attach_packed(spec: VaeSpec, device):
             gat, sca = buf[o:o + k], buf[o + k:o + 2 * k]
             o += 2 * k
             c.wfwd, c.wbwd = (sca, gat) if c.transposed else (gat, sca)
+            c.wk = gat
             spec.pack_items[part].append(
                 cv_conv_pack(w.data_ptr(), gat.data_ptr(), sca.data_ptr(), w.shape[0], w.shape[1], w.shape[2],
                              w.shape[3]))
@@ -801,7 +803,7 @@ class Workspace:
                 P.add("cv_convt_output_loss", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep, self.bn_dec[-1].cv(True), x,
                       self.xhat, self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
                 return
-            P.add("cv_conv_forward", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep)
+            P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wk, c.mod.bias, self.y_dec[li], ep)
             cur = self.y_dec[li]
         if output == "xhat":
             P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)
@@ -865,7 +867,7 @@ class Workspace:
             gout = operand(self.g_enc[li], XF_BNBWD, self.bn_enc[li].cv(True), y=self.y_enc[li])
             if li > 0:
                 ep = ep_bwd(self.bn_enc[li - 1], self.y_enc[li - 1], True)
-                P.add("cv_conv_backward_data", g, gout, c.wbwd, self.g_enc[li - 1], ep)
+                P.add("cv_conv_backward_data_kpack", g, gout, c.wbwd, c.wk, self.g_enc[li - 1], ep)
                 xin = operand(self.y_enc[li - 1], XF_BNRELU, self.bn_enc[li - 1].cv(True))
             else:
                 if dx is not None:

@@ -139,6 +139,17 @@ int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* wpacked
 int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* wpacked,
                           float* gin, const cv_epilogue* ep, cv_stream_t stream);
 
+/* The same two calls given also wkpack = the `gather` packing Wg[tap][cb][cs] of the same weight (the
+ * k-contiguous image of the SCATTER contraction's B operand; NULL allowed).  Results are those of
+ * cv_conv_forward / cv_conv_backward_data; with wkpack
+ * the library may run a stride-2 SCATTER contraction (Conv2d backward-data, ConvTranspose2d forward) as one
+ * class-fused direct launch that stages the small-grid operand in LDS once (cv_direct.hip) instead of one
+ * implicit GEMM per stride-parity class.  Replaces the same ATen calls (vae.py:15-46, 113-156). */
+int cv_conv_forward_kpack(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* wkpack,
+                          const float* bias, float* out, const cv_epilogue* ep, cv_stream_t stream);
+int cv_conv_backward_data_kpack(const cv_conv* g, const cv_operand* gout, const float* wpacked,
+                                const float* wkpack, float* gin, const cv_epilogue* ep, cv_stream_t stream);
+
 /* dw += sum_pixels T(x) (x) T(dy).  Replaces the grad_weight half of aten::convolution_backward.
  * gbias (optional, Conv2d only) += sum_pixels T(dy).  The pixel sum is split over workgroups
  * (split_k <= 0: automatic); the partial tiles go to `work` (cv_conv_wgrad_workspace_bytes) and one
@@ -515,6 +526,8 @@ int cv_version(void);
 /* test hook: 1 routes every conv/linear GEMM to the generic implicit-GEMM kernel instead of the
  * specialised core (both compute the same contraction); returns the previous setting */
 int cv_debug_force_generic_gemm(int on);
+/* test hook: launches of the class-fused direct SCATTER kernel (cv_conv_*_kpack) since the last reset */
+int cv_debug_direct_count(int reset);
 
 /* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
  * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least
