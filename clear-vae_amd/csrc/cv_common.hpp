@@ -88,6 +88,10 @@ int edge_bwd(const Geo& g, const cv_operand* gout, const float* wg, float* gin, 
 // call is not one it serves
 int direct_scatter(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,
                    const cv_epilogue* ep, hipStream_t st, int mma);
+// the same for a stride-2 GATHER (Conv2d forward / ConvTranspose2d backward-data); wk = the `scatter` packing
+// [tap][cs][cb]
+int direct_gather(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,
+                  const cv_epilogue* ep, hipStream_t st, int mma);
 
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {

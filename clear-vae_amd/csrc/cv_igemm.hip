@@ -1053,6 +1053,10 @@ static int gather_split(long tiles, int ktiles) {
   return s;
 }
 
+// the other packing of the current call's weights (cv_conv_*_kpack: the k-contiguous B image of the direct
+// kernels, [tap][co][ci]), else null
+static thread_local const float* g_wk = nullptr;
+
 // GATHER with small = rows.  `in` is the big-grid tensor; w is packed [tap][cb][cs].
 // CV_FUSED_OUT=1: the ConvT-to-image forward and the decoder output in one launch with a grid-wide wait for the
 // output BN's sums (edge_scatter_out); measured slower (MNIST 0.582 -> 0.616 ms/step: the fused launch needs a
@@ -1077,6 +1081,8 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
   if (!g_force_generic) {
     const int er = edge_gather(g, in, w, bias, out, ep, st);
     if (er >= 0) return er;
+    const int dr = direct_gather(g, in, g_wk, bias, out, ep, st, mma);
+    if (dr >= 0) return dr;
   }
   const int nr = narrow_gather(g, in, w, bias, out, ep, st);
   if (nr >= 0) return nr;
@@ -1126,9 +1132,6 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
   }
   return launch(a, BM_, BN_, 1, st);
 }
-
-// the k-contiguous packing [tap][cb][cs] of the current call's weights (cv_conv_*_kpack), else null
-static thread_local const float* g_wk = nullptr;
 
 // SCATTER with big = rows. `in` is the small-grid tensor; w is packed [tap][cs][cb].
 static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const float* bias, float* out,
@@ -1524,6 +1527,17 @@ extern "C" int cv_conv_backward_deferred(const cv_conv* g, const cv_operand* gou
   const int r = cv_conv_backward_data(g, gout, wpacked, gin, ep, stream);
   if (r) return r;
   return cv_conv_backward_weight_deferred(g, in, gout, gweight, gbias, work, work_bytes, defer, stream);
+}
+
+extern "C" int cv_conv_backward_deferred_kpack(const cv_conv* g, const cv_operand* gout, const float* wpacked,
+                                               const float* wkpack, float* gin, const cv_epilogue* ep,
+                                               const cv_operand* in, float* gweight, float* gbias, float* work,
+                                               size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t stream) {
+  g_wk = wkpack;
+  const int r = cv_conv_backward_deferred(g, gout, wpacked, gin, ep, in, gweight, gbias, work, work_bytes, defer,
+                                          stream);
+  g_wk = nullptr;
+  return r;
 }
 
 // ---------------------------------------------------------------- linear layers

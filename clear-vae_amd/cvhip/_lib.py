@@ -172,6 +172,11 @@ _SIGS = {
         [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, _P(cv_epilogue), _P(cv_operand), c_void_p, c_void_p,
          c_void_p, c_size_t, _P(cv_wgrad_defer), c_void_p],
     ),
+    "cv_conv_backward_deferred_kpack": (
+        c_int,
+        [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), _P(cv_operand), c_void_p,
+         c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer), c_void_p],
+    ),
     "cv_linear_backward_weight_deferred": (
         c_int,
         [_P(cv_linear), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer),
@@ -333,6 +338,7 @@ _SIGS = {
     "cv_version": (c_int, []),
     "cv_debug_force_generic_gemm": (c_int, [c_int]),
     "cv_debug_direct_count": (c_int, [c_int]),
+    "cv_debug_direct_minwg": (c_int, [c_int]),
     "cv_gemm_workspace_bytes": (c_size_t, []),
     "cv_set_gemm_workspace": (c_int, [c_void_p, c_size_t]),
 }

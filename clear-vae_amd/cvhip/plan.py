@@ -56,7 +56,6 @@ class ConvSpec:
     # GEMM-native weight copies (cv_pack_conv_weights): read by the forward / backward-data launch
     wfwd: object = None
     wbwd: object = None
-    wk: object = None  # the `gather` packing Wg[tap][cb][cs]: the k-contiguous B image of the SCATTER contraction
     mma: int = 0  # CV_MMA_* operand precision of this layer's GEMMs (cvhip.set_precision)
 
     def geom(self, n: int) -> cv_conv:
@@ -288,7 +287,6 @@ def attach_packed(spec: VaeSpec, device):
             gat, sca = buf[o:o + k], buf[o + k:o + 2 * k]
             o += 2 * k
             c.wfwd, c.wbwd = (sca, gat) if c.transposed else (gat, sca)
-            c.wk = gat
             spec.pack_items[part].append(
                 cv_conv_pack(w.data_ptr(), gat.data_ptr(), sca.data_ptr(), w.shape[0], w.shape[1], w.shape[2],
                              w.shape[3]))
@@ -645,14 +643,14 @@ class Workspace:
     # image-side ConvTranspose2d; CVHIP_FUSED_EDGE_BWD=0: the two calls)
     FUSED_EDGE_BWD = os.environ.get("CVHIP_FUSED_EDGE_BWD", "1") != "0"
 
-    def _conv_backward(self, P: "Program", geom, gout, wpacked, gin, ep, xin, gw, key, defer):
+    def _conv_backward(self, P: "Program", geom, gout, wpacked, wkpack, gin, ep, xin, gw, key, defer):
         if defer is None or not self.FUSED_EDGE_BWD:
-            P.add("cv_conv_backward_data", geom, gout, wpacked, gin, ep)
+            P.add("cv_conv_backward_data_kpack", geom, gout, wpacked, wkpack, gin, ep)
             self._wgrad_call(P, "conv", geom, xin, gout, gw, None, key, defer)
             return
         buf = self._defer_buf("conv", geom, key)
-        P.add("cv_conv_backward_deferred", geom, gout, wpacked, gin, ep, xin, gw, None, buf, buf.numel() * 4,
-              defer.next())
+        P.add("cv_conv_backward_deferred_kpack", geom, gout, wpacked, wkpack, gin, ep, xin, gw, None, buf,
+              buf.numel() * 4, defer.next())
 
     def _views(self, which) -> list:
         """BN layers by name ('all', 'enc', 'dec') or an explicit list of BNViews (a gradient bucket's)."""
@@ -715,7 +713,7 @@ class Workspace:
             else:
                 op = operand(cur, XF_BNRELU, self.bn_enc[li - 1].cv(train))
             ep = ep_fwd(self.bn_enc[li]) if train else ep_none()
-            P.add("cv_conv_forward", g, op, c.wfwd, c.mod.bias, self.y_enc[li], ep)
+            P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, self.y_enc[li], ep)
             cur = self.y_enc[li]
         # heads (Linear on the NCHW-flattened activation)
         C, Hh, Wh = sp.feat
@@ -803,7 +801,7 @@ class Workspace:
                 P.add("cv_convt_output_loss", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep, self.bn_dec[-1].cv(True), x,
                       self.xhat, self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
                 return
-            P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wk, c.mod.bias, self.y_dec[li], ep)
+            P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, self.y_dec[li], ep)
             cur = self.y_dec[li]
         if output == "xhat":
             P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)
@@ -820,11 +818,11 @@ class Workspace:
             if li > 0:
                 ep = ep_bwd(self.bn_dec[li - 1], self.y_dec[li - 1], sp.dec[li - 1].relu)
                 xin = operand(self.y_dec[li - 1], XF_BNRELU, self.bn_dec[li - 1].cv(True))
-                self._conv_backward(P, g, gout, c.wbwd, self.g_dec[li - 1], ep, xin, param_grad(c.mod.weight),
-                                    ("dec", li), defer)
+                self._conv_backward(P, g, gout, c.wbwd, c.wfwd, self.g_dec[li - 1], ep, xin,
+                                    param_grad(c.mod.weight), ("dec", li), defer)
                 continue
             else:
-                P.add("cv_conv_backward_data", g, gout, c.wbwd, self.gah, ep_none())
+                P.add("cv_conv_backward_data_kpack", g, gout, c.wbwd, c.wfwd, self.gah, ep_none())
                 xin = operand(self.ah)
             self._wgrad_call(P, "conv", g, xin, gout, param_grad(c.mod.weight), None, ("dec", li), defer)
         Cu, Hu, Wu = sp.unflat
@@ -867,7 +865,7 @@ class Workspace:
             gout = operand(self.g_enc[li], XF_BNBWD, self.bn_enc[li].cv(True), y=self.y_enc[li])
             if li > 0:
                 ep = ep_bwd(self.bn_enc[li - 1], self.y_enc[li - 1], True)
-                P.add("cv_conv_backward_data_kpack", g, gout, c.wbwd, c.wk, self.g_enc[li - 1], ep)
+                P.add("cv_conv_backward_data_kpack", g, gout, c.wbwd, c.wfwd, self.g_enc[li - 1], ep)
                 xin = operand(self.y_enc[li - 1], XF_BNRELU, self.bn_enc[li - 1].cv(True))
             else:
                 if dx is not None:

@@ -139,12 +139,14 @@ int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* wpacked
 int cv_conv_backward_data(const cv_conv* g, const cv_operand* gout, const float* wpacked,
                           float* gin, const cv_epilogue* ep, cv_stream_t stream);
 
-/* The same two calls given also wkpack = the `gather` packing Wg[tap][cb][cs] of the same weight (the
- * k-contiguous image of the SCATTER contraction's B operand; NULL allowed).  Results are those of
- * cv_conv_forward / cv_conv_backward_data; with wkpack
- * the library may run a stride-2 SCATTER contraction (Conv2d backward-data, ConvTranspose2d forward) as one
- * class-fused direct launch that stages the small-grid operand in LDS once (cv_direct.hip) instead of one
- * implicit GEMM per stride-parity class.  Replaces the same ATen calls (vae.py:15-46, 113-156). */
+/* The same calls given also wkpack = the OTHER packing of the same weight (the one wpacked is not: for a
+ * stride-2 SCATTER contraction — Conv2d backward-data, ConvTranspose2d forward — the `gather` packing
+ * [tap][cb][cs]; for a GATHER — Conv2d forward, ConvTranspose2d backward-data — the `scatter` packing
+ * [tap][cs][cb]; i.e. the contraction's B operand k-contiguous per output channel; NULL allowed).  Results are
+ * those of the calls without it; with it the library may run the contraction as one direct launch that stages
+ * the operand's band in LDS once per workgroup and walks all taps (and, for SCATTER, all four stride-parity
+ * classes) from there (cv_direct.hip) instead of implicit GEMMs that re-load it per tap.  Replaces the same
+ * ATen calls (vae.py:15-46, 113-156). */
 int cv_conv_forward_kpack(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* wkpack,
                           const float* bias, float* out, const cv_epilogue* ep, cv_stream_t stream);
 int cv_conv_backward_data_kpack(const cv_conv* g, const cv_operand* gout, const float* wpacked,
@@ -182,6 +184,11 @@ int cv_conv_backward_weight_deferred(const cv_conv* g, const cv_operand* in, con
 int cv_conv_backward_deferred(const cv_conv* g, const cv_operand* gout, const float* wpacked, float* gin,
                               const cv_epilogue* ep, const cv_operand* in, float* gweight, float* gbias, float* work,
                               size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t stream);
+/* cv_conv_backward_deferred with the other packing of the weight (see cv_conv_forward_kpack) */
+int cv_conv_backward_deferred_kpack(const cv_conv* g, const cv_operand* gout, const float* wpacked,
+                                    const float* wkpack, float* gin, const cv_epilogue* ep, const cv_operand* in,
+                                    float* gweight, float* gbias, float* work, size_t work_bytes,
+                                    cv_wgrad_defer* defer, cv_stream_t stream);
 
 /* ---- fully connected layers (nn.Linear heads vae.py:27-30; decoder Linear vae.py:33) ----
  * A linear layer whose input (or output) is the NCHW-flattened view of an NHWC activation with
@@ -526,8 +533,11 @@ int cv_version(void);
 /* test hook: 1 routes every conv/linear GEMM to the generic implicit-GEMM kernel instead of the
  * specialised core (both compute the same contraction); returns the previous setting */
 int cv_debug_force_generic_gemm(int on);
-/* test hook: launches of the class-fused direct SCATTER kernel (cv_conv_*_kpack) since the last reset */
+/* test hook: launches of the direct conv kernel (cv_conv_*_kpack) since the last reset */
 int cv_debug_direct_count(int reset);
+/* test hook: the fewest workgroups for which a stride-2 conv takes the direct kernel (default 256; smaller
+ * grids run the GEMM core); returns the previous setting (-1: not yet initialised) */
+int cv_debug_direct_minwg(int minwg);
 
 /* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
  * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least

@@ -13,8 +13,8 @@ BatchNorm after every conv renormalises, so the errors do not compound with dept
   * gradients against the plain fp64 oracle: whole-model relative L2 < 0.15 and median per-tensor < 0.15
     (measured 0.04-0.09 at N=32..128: at initialisation many BatchNorm outputs sit near 0, and a bf16 forward
     flips the ReLU of ~0.1% of them against fp64, each flip changing that element's whole upstream gradient);
-    test_bf16_step_mask_pinned removes both effects (the device's ReLU pattern pinned, the bf16 rounding
-    restated in the oracle) and holds every tensor at 1e-3 (median 1e-4);
+    test_bf16_step_mask_pinned removes the ReLU flips (the device's pattern pinned) and restates the bf16
+    rounding in the oracle, and holds every tensor to the fp32 floor of that function (_check_bf16_pinned);
   * the same step in fp32 on the same engine stays within the fp32 bar (1e-4), so the looser numbers
     are the bf16 operands' and nothing else;
   * kernel level (below): with bf16-representable operands the bf16 core matches an fp64 contraction at
@@ -103,9 +103,8 @@ def test_bf16_step_mask_pinned(arch, zt, C, n):
     (oracle/cpu_ref.py `bf16=`: the GEMM-core convs' input activation after its BN+ReLU, the weight, and the
     incoming gradient after the BN backward; fp64 accumulation) with the device's ReLU activity pinned
     (tests/maskpin.py).  What remains is fp32 accumulation order and the rare bf16 tie broken differently by an
-    fp32 vs fp64 pre-rounding value, so the bars are close to the fp32 ones: losses, heads and z within 1e-4
-    relative; every gradient tensor within max(1e-3, 8 x the floor of the same bf16-rounding oracle run in fp32),
-    the median tensor within 1e-4."""
+    fp32 vs fp64 pre-rounding value, which the function amplifies (_check_bf16_pinned): heads and z within 1e-4
+    relative, losses within max(1e-4 relative, 2 x the fp32 oracle's own deviation), gradients at the fp32 floor."""
     from cvhip import rng
     from cvhip.engine import ClearStep
     from cvhip.plan import set_precision
@@ -136,23 +135,40 @@ def test_bf16_step_mask_pinned(arch, zt, C, n):
     o, o32 = oracle(torch.float64), oracle(torch.float32)
     for i, k in enumerate(("rec", "kl_c", "kl_s", "c_loss", "s_loss")):
         ref = float(o[k])
-        assert abs(float(losses[i]) - ref) <= 1e-4 * max(abs(ref), 1e-3), (k, float(losses[i]), ref)
+        floor = abs(float(o32[k]) - ref)
+        assert abs(float(losses[i]) - ref) <= max(1e-4 * max(abs(ref), 1e-3), PIN_FLOOR_X * floor), (
+            k, float(losses[i]), ref, floor)
     ref_heads = torch.cat([o[k] for k in ("mu_c", "logvar_c", "mu_s", "logvar_s")], dim=1).detach()
     assert _rel(heads, ref_heads) < 1e-4 and _rel(z, o["z"].detach()) < 1e-4
+    _check_bf16_pinned({k: grads[k] for k in o["grads"]}, o["grads"], o32["grads"], arch, f"{arch} n={n}")
+
+
+# The bf16-rounding function is ill-conditioned in a way fp32 is not: an operand within fp32 rounding of a bf16
+# rounding midpoint rounds either way, each such flip moves that operand by 2^-8, and the flips multiply layer
+# after layer.  So even the oracle's own fp32 evaluation of the identical function (same masks, same rounding
+# points) lands 1e-3 - 6e-3 from its fp64 evaluation per gradient tensor (measured; the fp32 "floor").  The device
+# can be no closer; the bars hold it to that floor: every tensor within max(1e-3, PIN_FLOOR_X x its floor) and the
+# median tensor within max(1e-4, PIN_FLOOR_X x the median floor).  (A wrong bf16 weight gradient on any tensor
+# is off by O(1), far outside.)
+PIN_FLOOR_X = 2.0
+
+
+def _check_bf16_pinned(got, ref64, ref32, arch, what):
     rels, over = [], []
-    for k, g_ref in o["grads"].items():
+    for k, g_ref in ref64.items():
         if _bias_before_bn(k, arch):
             continue
-        r = _rel(grads[k], g_ref.detach())
-        floor = _rel(o32["grads"][k].detach().double(), g_ref.detach())
+        r = _rel(got[k], g_ref.detach())
+        floor = _rel(ref32[k].detach().double(), g_ref.detach())
         rels.append((r, k, floor))
-        if r >= max(1e-3, 8.0 * floor):
+        if r >= max(1e-3, PIN_FLOOR_X * floor):
             over.append((k, r, floor))
     rels.sort()
     med = rels[len(rels) // 2][0]
-    print(f"\n{arch} n={n} bf16 pinned: median {med:.2e}; worst (rel, tensor, fp32 floor): "
+    fmed = sorted(f for _, _, f in rels)[len(rels) // 2]
+    print(f"\n{what} bf16 pinned: median {med:.2e} (floor median {fmed:.2e}); worst (rel, tensor, fp32 floor): "
           + ", ".join(f"({r:.1e}, {k}, {f:.1e})" for r, k, f in rels[-3:]))
-    assert med < 1e-4, (med, rels[-3:])
+    assert med < max(1e-4, PIN_FLOOR_X * fmed), (med, fmed, rels[-3:])
     assert not over, over
 
 
