@@ -10,15 +10,16 @@
 //             per-group torch.randn), z_s[s] = mu_s + eps * exp(lv_s/2)
 //   backward: KL over the m group rows, the B/m adjustment of rec / kl_s (trainer.py:322-324, 345-347),
 //             the reparam chain summed per segment, then back through the evidence to every member.
-// Batches are small (n <= 4096, d <= 64): one workgroup of 1024 threads does the whole problem, so the
-// segmentation needs no grid-wide synchronisation and every reduction has a fixed order.
+// One workgroup of 1024 threads does the whole problem (n <= 32768, d <= 64; labels staged in LDS up to 4096), so
+// the segmentation needs no grid-wide synchronisation and every reduction has a fixed order.
 #include "cv_common.hpp"
 
 namespace cv {
 
 constexpr int GR_NT = 1024;
 constexpr int GR_NW = GR_NT / 64;
-constexpr int GR_MAXN = 4096;
+constexpr int GR_MAXN = 4096;     // largest batch whose labels the forward stages in LDS
+constexpr int GR_MAXBIG = 32768;  // largest batch at all (the segmentation is O(n^2) in one workgroup)
 constexpr int GR_MAXD = 64;
 
 struct GroupLayout {
@@ -99,13 +100,18 @@ struct GroupFwd {
   float* z;
 };
 
+// BIG: batches above GR_MAXN (the reference has no cap, vae.py:159-223): the labels are read from global memory
+// (L2-resident) instead of an LDS copy; every other step already walks the batch in workgroup strides
+template <bool BIG>
 __global__ __launch_bounds__(GR_NT) void group_forward_kernel(const GroupFwd A) {
-  __shared__ int64_t lab[GR_MAXN];
+  __shared__ int64_t lab_s[BIG ? 1 : GR_MAXN];
   __shared__ int scan[GR_NW];
   const int n = A.n, d = A.d, t = threadIdx.x;
   const GroupLayout& L = A.L;
   const uint64_t off = (A.offset && !A.eps) ? A.offset[0] : 0;
-  for (int s = t; s < n; s += GR_NT) lab[s] = A.label[s];
+  const int64_t* lab = BIG ? A.label : lab_s;
+  if (!BIG)
+    for (int s = t; s < n; s += GR_NT) lab_s[s] = A.label[s];
   __syncthreads();
   // 1. group-order position of every sample
   for (int s = t; s < n; s += GR_NT) {
@@ -337,8 +343,8 @@ extern "C" int cv_group_forward(int mode, const float* mu_c, const float* lv_c, 
                                 cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(mode == CV_GROUP_MLVAE || mode == CV_GROUP_GVAE, "group_forward: mode %d (MLVAE=0, GVAE=1)", mode);
-  CV_REQUIRE(mu_c && lv_c && label && work && n > 0 && n <= GR_MAXN && d > 0 && d <= GR_MAXD && ld >= d,
-             "group_forward: bad args (n <= %d, d <= %d)", GR_MAXN, GR_MAXD);
+  CV_REQUIRE(mu_c && lv_c && label && work && n > 0 && n <= GR_MAXBIG && d > 0 && d <= GR_MAXD && ld >= d,
+             "group_forward: bad args (n <= %d, d <= %d)", GR_MAXBIG, GR_MAXD);
   CV_REQUIRE(!z || (mu_s && lv_s && lds >= d && (eps || offset)),
              "group_forward: z needs mu_s / lv_s and injected eps or a device offset counter");
   CV_REQUIRE(!eps || ld_eps >= 2 * d, "group_forward: eps rows hold 2d values");
@@ -360,7 +366,8 @@ extern "C" int cv_group_forward(int mode, const float* mu_c, const float* lv_c, 
   A.seed = seed;
   A.offset = offset;
   A.z = z;
-  hipLaunchKernelGGL(group_forward_kernel, dim3(1), dim3(GR_NT), 0, S(stream), A);
+  if (n > GR_MAXN) hipLaunchKernelGGL(group_forward_kernel<true>, dim3(1), dim3(GR_NT), 0, S(stream), A);
+  else hipLaunchKernelGGL(group_forward_kernel<false>, dim3(1), dim3(GR_NT), 0, S(stream), A);
   CV_LAUNCH_CHECK("group_forward");
   return 0;
 }
@@ -370,7 +377,7 @@ extern "C" int cv_group_backward(int mode, const float* heads, const float* z, c
                                  const double* rec_in, float* dheads, float* losses, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(mode == CV_GROUP_MLVAE || mode == CV_GROUP_GVAE, "group_backward: mode %d", mode);
-  CV_REQUIRE(heads && z && dz && work && anneal_step && dheads && losses && n > 0 && n <= GR_MAXN && d > 0 &&
+  CV_REQUIRE(heads && z && dz && work && anneal_step && dheads && losses && n > 0 && n <= GR_MAXBIG && d > 0 &&
                  d <= GR_MAXD,
              "group_backward: bad args");
   GroupBwd A;
@@ -398,7 +405,7 @@ extern "C" int cv_group_evidence_backward(int mode, const float* mu_c, const flo
                                           float* dlv_c, int ldo, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(mode == CV_GROUP_MLVAE || mode == CV_GROUP_GVAE, "group_evidence_backward: mode %d", mode);
-  CV_REQUIRE(mu_c && lv_c && work && dmu_c && dlv_c && n > 0 && n <= GR_MAXN && d > 0 && d <= GR_MAXD &&
+  CV_REQUIRE(mu_c && lv_c && work && dmu_c && dlv_c && n > 0 && n <= GR_MAXBIG && d > 0 && d <= GR_MAXD &&
                  ld >= d && ldo >= d,
              "group_evidence_backward: bad args");
   EvidenceBwd A;

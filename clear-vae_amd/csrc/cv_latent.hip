@@ -246,7 +246,9 @@ struct NtArgs {
 };
 
 constexpr int NT_ROWS = 4;   // rows (waves) per 256-thread block
-constexpr int NT_MAXN = 4096;
+constexpr int NT_MAXN = 4096;      // largest batch whose row norms the global-walk kernels stage in LDS
+constexpr int NT_MAXBIG = 1 << 17;  // largest batch at all (the BIG kernels: each gradient block re-counts the
+                                    // finite rows, O(n) per block)
 
 // similarity of row i (theta_i) and column j
 template <int DM>
@@ -335,14 +337,27 @@ __device__ __forceinline__ float row_norm(const Branch& b, int r, int d) {
   return sqrtf(s);
 }
 
+// the norm of a row already in registers: the same operations, in the same order, as row_norm
 template <int DM>
+__device__ __forceinline__ float reg_norm(const float* m, int d) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) s += m[k] * m[k];
+  return sqrtf(s);
+}
+
+// Global-walk kernels (the branch does not fit the LDS-staged variants).  BIG: batches above NT_MAXN (the
+// reference has no cap, losses.py:98-137): the row norms are recomputed from the loaded rows instead of being
+// staged in LDS (bit-identical: reg_norm), so the kernels need no per-batch LDS at all.
+template <int DM, bool BIG>
 __global__ __launch_bounds__(256) void ntxent_rows_kernel(const NtArgs A) {
-  __shared__ float nrm[NT_MAXN];
+  __shared__ float nrm[BIG ? 1 : NT_MAXN];
   const Branch& b = A.br[blockIdx.y];
   const int n = A.n, d = A.d;
   const bool cosine = A.sim == CV_SIM_COSINE;
   const bool need_lv = !(A.sim == CV_SIM_COSINE || A.sim == CV_SIM_L2);
-  if (cosine)
+  if (cosine && !BIG)
     for (int j = threadIdx.x; j < n; j += 256) nrm[j] = fmaxf(row_norm(b, j, d), 1e-8f);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -350,13 +365,14 @@ __global__ __launch_bounds__(256) void ntxent_rows_kernel(const NtArgs A) {
   if (i >= n) return;
   float mi[DM], li[DM], mj[DM], lj[DM];
   load_theta<DM>(b, i, d, mi, li, need_lv);
-  const float ni = cosine ? nrm[i] : 1.f;
+  const float ni = cosine ? (BIG ? fmaxf(reg_norm<DM>(mi, d), 1e-8f) : nrm[i]) : 1.f;
   const int64_t lab = A.label[i];
   float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
   for (int j = lane; j < n; j += 64) {
     if (j == i) continue;
     load_theta<DM>(b, j, d, mj, lj, need_lv);
-    const float s = sim_ij<DM>(A.sim, mi, li, ni, mj, lj, cosine ? nrm[j] : 1.f, d) / A.tau;
+    const float nj = cosine ? (BIG ? fmaxf(reg_norm<DM>(mj, d), 1e-8f) : nrm[j]) : 1.f;
+    const float s = sim_ij<DM>(A.sim, mi, li, ni, mj, lj, nj, d) / A.tau;
     lse_merge(ma, sa, s, 1.f);
     const bool pos = b.ps ? (A.label[j] != lab) : (A.label[j] == lab);
     if (pos) lse_merge(mp, sp, s, 1.f);
@@ -430,10 +446,10 @@ __device__ __forceinline__ void sim_grad_row(int sim, const float* mi, const flo
     }
 }
 
-template <int DM>
+template <int DM, bool BIG>
 __global__ __launch_bounds__(256) void ntxent_grad_kernel(const NtArgs A) {
-  __shared__ float nrm[NT_MAXN];
-  __shared__ float rawn[NT_MAXN];
+  __shared__ float nrm[BIG ? 1 : NT_MAXN];
+  __shared__ float rawn[BIG ? 1 : NT_MAXN];
   __shared__ float scratch[16];
   __shared__ double dscratch[16];
   const Branch& b = A.br[blockIdx.y];
@@ -449,7 +465,7 @@ __global__ __launch_bounds__(256) void ntxent_grad_kernel(const NtArgs A) {
       cnt += 1.f;
       lsum += (double)l;
     }
-    if (cosine) {
+    if (cosine && !BIG) {
       const float r = row_norm(b, j, d);
       rawn[j] = r;
       nrm[j] = fmaxf(r, 1e-8f);
@@ -471,15 +487,16 @@ __global__ __launch_bounds__(256) void ntxent_grad_kernel(const NtArgs A) {
   load_theta<DM>(b, i, d, mi, li, need_lv);
 #pragma unroll
   for (int k = 0; k < DM; ++k) { gm[k] = 0.f; gl[k] = 0.f; }
-  const float ni = cosine ? nrm[i] : 1.f;
-  const bool clamped_i = cosine && !(rawn[i] > 1e-8f);
+  const float rni = (cosine && BIG) ? reg_norm<DM>(mi, d) : 0.f;
+  const float ni = cosine ? (BIG ? fmaxf(rni, 1e-8f) : nrm[i]) : 1.f;
+  const bool clamped_i = cosine && !((BIG ? rni : rawn[i]) > 1e-8f);
   const int64_t lab = A.label[i];
   const float la_i = b.lse[i], lp_i = b.lse[n + i];
   const bool fin_i = isfinite(la_i - lp_i);
   for (int j = lane; j < n; j += 64) {
     if (j == i) continue;
     load_theta<DM>(b, j, d, mj, lj, need_lv);
-    const float nj = cosine ? nrm[j] : 1.f;
+    const float nj = cosine ? (BIG ? fmaxf(reg_norm<DM>(mj, d), 1e-8f) : nrm[j]) : 1.f;
     const float S = sim_ij<DM>(A.sim, mi, li, ni, mj, lj, nj, d);
     const float s = S / A.tau;
     const bool pos = b.ps ? (A.label[j] != lab) : (A.label[j] == lab);
@@ -1106,19 +1123,21 @@ static int ntxent_launch(const NtArgs& a, int nbr, bool rows, hipStream_t st) {
     CV_LAUNCH_CHECK("latent_combine");
   }
   dim3 grid(cdiv(a.n, NT_ROWS), nbr);
-  if (a.d <= 8) {
-    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<8>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(ntxent_grad_kernel<8>, grid, dim3(256), 0, st, a);
-  } else if (a.d <= 16) {
-    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<16>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(ntxent_grad_kernel<16>, grid, dim3(256), 0, st, a);
-  } else if (a.d <= 32) {
-    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<32>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(ntxent_grad_kernel<32>, grid, dim3(256), 0, st, a);
+#define CV_NT_GLOBAL(DM_, BIG_)                                                          \
+  if (rows) hipLaunchKernelGGL((ntxent_rows_kernel<DM_, BIG_>), grid, dim3(256), 0, st, a); \
+  else hipLaunchKernelGGL((ntxent_grad_kernel<DM_, BIG_>), grid, dim3(256), 0, st, a);
+#define CV_NT_DM(BIG_)                           \
+  if (a.d <= 8) { CV_NT_GLOBAL(8, BIG_) }        \
+  else if (a.d <= 16) { CV_NT_GLOBAL(16, BIG_) } \
+  else if (a.d <= 32) { CV_NT_GLOBAL(32, BIG_) } \
+  else { CV_NT_GLOBAL(64, BIG_) }
+  if (a.n > NT_MAXN) {
+    CV_NT_DM(true)
   } else {
-    if (rows) hipLaunchKernelGGL(ntxent_rows_kernel<64>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(ntxent_grad_kernel<64>, grid, dim3(256), 0, st, a);
+    CV_NT_DM(false)
   }
+#undef CV_NT_DM
+#undef CV_NT_GLOBAL
   CV_LAUNCH_CHECK(rows ? "ntxent_rows" : "ntxent_grad");
   return 0;
 }
@@ -1216,7 +1235,7 @@ extern "C" int cv_mse_sum(const float* xhat, const float* x, int n, int per_samp
 static int ntxent_args(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
                        float temperature, int accumulate, NtArgs& a) {
   CV_REQUIRE(br && nbr >= 1 && nbr <= MAXBR && label && n > 0 && d > 0 && d <= 64, "ntxent: bad args (d<=64)");
-  CV_REQUIRE(n <= NT_MAXN, "ntxent: batch %d > %d", n, NT_MAXN);
+  CV_REQUIRE(n <= NT_MAXBIG, "ntxent: batch %d > %d", n, NT_MAXBIG);
   CV_REQUIRE(sim >= CV_SIM_COSINE && sim <= CV_SIM_MAHALANOBIS, "unimplemented similarity measure.");
   memset(&a, 0, sizeof(a));
   for (int i = 0; i < nbr; ++i) {

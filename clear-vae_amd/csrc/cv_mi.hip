@@ -153,7 +153,8 @@ __device__ __forceinline__ float mlp_bwd_row(const MlpLds<DM>& L, int dx, int h,
 }
 
 // ---------------------------------------------------------------- workspace
-constexpr int MI_MAXN = 4096;
+constexpr int MI_MAXN = 4096;      // largest batch of the one-workgroup device permutation (bitonic sort in LDS)
+constexpr int MI_MAXBIG = 1 << 20;  // largest batch at all (above MI_MAXN: mi_perm_big_kernel)
 #ifndef CV_MI_NB
 #define CV_MI_NB 64  // (64 row workgroups for the learning step measured +0.2 % on C3 over 32)
 #endif
@@ -233,6 +234,40 @@ __device__ __forceinline__ bool last_block(unsigned* ticket, int* flag) {
   return *flag != 0;
 }
 
+// ---------------------------------------------------------------- device permutation above MI_MAXN
+// CLUBSample's torch.randperm (mi_estimator.py:138) for batches the one-workgroup bitonic sort below cannot hold
+// (the reference has no cap): a keyed bijection of [0, n) evaluated per element — a 4-round balanced Feistel
+// network on 2h bits (2^2h >= n, h >= 1) with Philox round functions, restricted to [0, n) by cycle walking (at
+// most 4 expected steps: 2^2h < 4n).  Grid-stride, any number of workgroups; perm[i] and invperm[perm[i]] = i.
+__device__ __forceinline__ unsigned feistel(unsigned x, int h, uint64_t seed, uint64_t off) {
+  const unsigned mask = (1u << h) - 1u;
+  unsigned L = x >> h, R = x & mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const unsigned f = philox(seed, off ^ 0x9e3779b97f4a7c15ull, ((uint64_t)r << 32) | R).x & mask;
+    const unsigned nl = R;
+    R = L ^ f;
+    L = nl;
+  }
+  return (L << h) | R;
+}
+
+__global__ __launch_bounds__(256) void mi_perm_big_kernel(const MiArgs A) {
+  const int n = A.n;
+  MiWork W = mi_work(A.work, n);
+  const uint64_t off = A.offset ? A.offset[0] : 0;  // (read before mi_perm_kernel advances it)
+  int h = 1;
+  while ((1ll << (2 * h)) < (long long)n) ++h;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    unsigned x = (unsigned)i;
+    do {
+      x = feistel(x, h, A.seed, off);
+    } while (x >= (unsigned)n);
+    W.perm[i] = (int)x;
+    W.invperm[x] = i;
+  }
+}
+
 // ---------------------------------------------------------------- perm / column sums (1 x 1024)
 __global__ __launch_bounds__(1024) void mi_perm_kernel(const MiArgs A) {
   __shared__ unsigned int keys[MI_MAXN];
@@ -241,7 +276,9 @@ __global__ __launch_bounds__(1024) void mi_perm_kernel(const MiArgs A) {
   const int n = A.n, t = threadIdx.x;
   MiWork W = mi_work(A.work, n);
   const uint64_t off = A.offset ? A.offset[0] : 0;
-  if (A.kind == CV_MI_CLUBSAMPLE) {
+  if (A.kind == CV_MI_CLUBSAMPLE && !A.perm_in && n > MI_MAXN) {
+    // (mi_perm_big_kernel, launched before this one, wrote the permutation)
+  } else if (A.kind == CV_MI_CLUBSAMPLE) {
     if (A.perm_in) {
       for (int i = t; i < n; i += 1024) {
         const int p = (int)A.perm_in[i];
@@ -819,7 +856,7 @@ extern "C" int cv_mi_forward(int kind, const cv_mlp* mlp, const float* x, int ld
   clear_error();
   if (check_mlp(mlp)) return 1;
   CV_REQUIRE(kind == CV_MI_CLUBSAMPLE || kind == CV_MI_L1OUT, "mi: unknown estimator %d", kind);
-  CV_REQUIRE(x && y && work && n > 1 && n <= MI_MAXN, "mi_forward: bad args (2 <= n <= %d)", MI_MAXN);
+  CV_REQUIRE(x && y && work && n > 1 && n <= MI_MAXBIG, "mi_forward: bad args (2 <= n <= %d)", MI_MAXBIG);
   CV_REQUIRE(kind != CV_MI_CLUBSAMPLE || perm || offset, "mi_forward: CLUBSample needs perm or an RNG offset");
   MiArgs a;
   memset(&a, 0, sizeof(a));
@@ -829,6 +866,10 @@ extern "C" int cv_mi_forward(int kind, const cv_mlp* mlp, const float* x, int ld
   a.perm_in = perm; a.seed = seed; a.offset = perm ? nullptr : offset;
   a.work = work;
   a.mi_out = mi_out;
+  if (kind == CV_MI_CLUBSAMPLE && !perm && n > MI_MAXN) {
+    hipLaunchKernelGGL(mi_perm_big_kernel, dim3(cdiv(n, 256) < 256 ? cdiv(n, 256) : 256), dim3(256), 0, S(stream), a);
+    CV_LAUNCH_CHECK("mi_forward.perm_big");
+  }
   hipLaunchKernelGGL(mi_perm_kernel, dim3(1), dim3(1024), 0, S(stream), a);
   CV_LAUNCH_CHECK("mi_forward.perm");
   CV_MI_DISPATCH(mlp_dm(mlp), mi_rows_kernel, dim3(mi_row_blocks(n)), dim3(256), S(stream), a);
@@ -842,7 +883,7 @@ extern "C" int cv_mi_backward(int kind, const cv_mlp* mlp, const float* x, int l
                               float* dheads, int d, cv_stream_t stream) {
   clear_error();
   if (check_mlp(mlp)) return 1;
-  CV_REQUIRE(x && y && work && n > 1 && n <= MI_MAXN, "mi_backward: bad args");
+  CV_REQUIRE(x && y && work && n > 1 && n <= MI_MAXBIG, "mi_backward: bad args");
   CV_REQUIRE(!dheads || (heads && z && d == mlp->dx && d == mlp->dy), "mi_backward: chain mode needs heads, z, d");
   MiArgs a;
   memset(&a, 0, sizeof(a));

@@ -346,6 +346,84 @@ def contrastive_loss(mu, logvar, label, sim_fn, temperature, ps=False):
     return losses[torch.isfinite(losses)].mean()
 
 
+# ----------------------------------------------------------------------------- large batches
+# The reference's contrastive_loss and L1OutUB materialise [N, N, d] / [N, N, N] intermediates; at the batches
+# above the HIP kernels' one-workgroup caps (tests/test_gpu_bigbatch.py, N = 8192) those do not fit a host.
+# These restate the SAME per-row terms block by block (contrastive) or in closed form (L1Out); each is checked
+# against the literal restatement above at small N (tests/test_oracle_golden.py).
+
+
+def pairwise_rows(sim_fn, mu, logvar, rows):
+    """pairwise(sim_fn, mu, logvar)[rows, :] (losses.py:53-84 and :111-123) without the other rows: every
+    expression of `pairwise` with its row operand X[:, None] restricted to X[rows][:, None]."""
+    mr = mu[rows]
+    if sim_fn == "cosine":
+        return F.cosine_similarity(mu[None, :, :], mr[:, None, :], dim=-1)
+    if sim_fn == "l2":
+        return -((mu[None, :, :] - mr[:, None, :]) ** 2).sum(dim=-1)
+    lr = logvar[rows]
+    if sim_fn == "modified_l2":
+        var = (0.5 * (logvar[None, :, :] + lr[:, None, :])).exp()
+        return -((mu[None, :, :] - mr[:, None, :]) ** 2 / var).sum(dim=-1)
+    if sim_fn == "jeffrey":
+        k = mu.shape[1]
+        var, vr = logvar.exp(), lr.exp()
+        L, Lr = logvar.sum(dim=-1), lr.sum(dim=-1)
+        d2 = (mu[None, :, :] - mr[:, None, :]) ** 2
+        kl_rj = 0.5 * (L[None, :] - Lr[:, None] - k + (d2 / var[None, :, :]).sum(dim=-1)
+                       + (var[None, :, :] / (vr[:, None, :] + 1e-8)).sum(dim=-1))    # kl[i, j], i in rows
+        kl_jr = 0.5 * (Lr[:, None] - L[None, :] - k + (d2 / vr[:, None, :]).sum(dim=-1)
+                       + (vr[:, None, :] / (var[None, :, :] + 1e-8)).sum(dim=-1))    # kl[j, i]
+        return -(0.5 * (kl_rj + kl_jr))
+    if sim_fn == "mahalanobis":
+        var = 0.5 * (logvar.exp()[None, :, :] + lr.exp()[:, None, :])
+        return -((mu[None, :, :] - mr[:, None, :]) ** 2 / var).sum(dim=-1)
+    raise ValueError("unimplemented similarity measure.")
+
+
+def contrastive_rows(mu, logvar, label, sim_fn, temperature, ps, rows):
+    """The snn_loss row terms (losses.py:129-137) of `rows`: -LSE(pos/tau) + LSE(sim/tau), diagonal at -inf."""
+    sim = pairwise_rows(sim_fn, mu, logvar, rows)
+    lab_r = label[rows]
+    pair = (label[None, :] != lab_r[:, None]) if ps else (label[None, :] == lab_r[:, None])
+    diag = torch.zeros_like(sim, dtype=torch.bool)
+    diag[torch.arange(len(rows)), rows] = True
+    sim = sim.masked_fill(diag, float("-inf"))
+    pos = (pair.to(sim.dtype) * sim).masked_fill(~pair, float("-inf"))
+    return -logsumexp(pos / temperature, dim=1) + logsumexp(sim / temperature, dim=1)
+
+
+def contrastive_loss_blockwise(mu, logvar, label, sim_fn, temperature, ps=False, block=128):
+    """contrastive_loss (losses.py:98-126: the mean over the finite rows) accumulated block by block, with the
+    gradient w.r.t. mu / logvar (leaves requiring grad) back-propagated per block so only one block's graph is
+    alive: returns the loss (a detached scalar); grads land in mu.grad / logvar.grad."""
+    n = mu.shape[0]
+    blocks = [torch.arange(i, min(n, i + block)) for i in range(0, n, block)]
+    with torch.no_grad():
+        terms = torch.cat([contrastive_rows(mu, logvar, label, sim_fn, temperature, ps, r) for r in blocks])
+    finite = torch.isfinite(terms)
+    nf = int(finite.sum())
+    loss = terms[finite].sum() / nf
+    if mu.requires_grad or (logvar is not None and logvar.requires_grad):
+        for r in blocks:
+            t = contrastive_rows(mu, logvar, label, sim_fn, temperature, ps, r)
+            t[torch.isfinite(t)].sum().div(nf).backward()
+    return loss
+
+
+def l1out_closed(M, x, y):
+    """L1OutUB.forward (mi_estimator.py:170-191) in closed form: the [N,N,N] broadcast of all_probs[N,N] with
+    diag_mask[N,N,1] makes negative[b,c] = all_probs[b,c] + log((N-1) + e^-20) - log(N-1) (the last log of a
+    float32 tensor, :188), and the mean over (b, c) of all_probs is a row sum of O(N d) moments."""
+    n = y.shape[0]
+    mu, lv = mlp_forward(M, x)
+    positive = (-((mu - y) ** 2) / 2.0 / lv.exp() - lv / 2.0).sum(dim=-1)
+    sy, sy2 = y.sum(dim=0), (y * y).sum(dim=0)
+    rows = (-(sy2[None, :] - 2.0 * mu * sy[None, :] + n * mu ** 2) / 2.0 / lv.exp() - n * lv / 2.0).sum(dim=-1)
+    delta = math.log((n - 1) + math.exp(-20.0)) - float((torch.tensor(n) - 1.0).log())
+    return positive.mean() - rows.sum() / (n * n) - delta
+
+
 def mlp_forward(M, x):
     """q(y|x) MLPs (mi_estimator.py:111-127)"""
     mu = F.linear(F.relu(F.linear(x, M["p_mu.0.weight"], M["p_mu.0.bias"])), M["p_mu.2.weight"], M["p_mu.2.bias"])

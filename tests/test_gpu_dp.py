@@ -87,7 +87,6 @@ def _rel(a, b):
 def _check_pinned(res, shard_step, arch, precision="fp32"):
     """The averaged gradient (res[0]["grad"], = res[1]'s) against the mean of the per-shard mask-pinned oracle
     gradients: shard_step(r, dtype, masks) -> oracle output on rank r's shard."""
-    med_tol, worst_tol = PIN[precision]
     outs = {dt: [shard_step(r, dt, masks_from_numpy(res[r]["masks"])) for r in (0, 1)]
             for dt in (torch.float64, torch.float32)}
     if precision == "bf16":  # the bf16 bars (tests/test_gpu_bf16.py _check_bf16_pinned: the fp32 floor)
@@ -98,6 +97,7 @@ def _check_pinned(res, shard_step, arch, precision="fp32"):
         _check_bf16_pinned({k: torch.tensor(v) for k, v in res[0]["grad"].items()}, mean[torch.float64],
                            mean[torch.float32], arch, "DP world 2")
         return
+    med_tol, worst_tol = PIN[precision]
     rels, over = [], []
     for k, g in res[0]["grad"].items():
         if _bias_before_bn(k, arch):

@@ -3,7 +3,8 @@ code/src/trainer.py:291-353) against the fp64 oracle (oracle/cpu_ref.group_evide
 the real reference by tests/golden/vae*_gvae*.npz / vae*_mlvae.npz).
 
 Module path: accumulate_group_evidence (cv_group_forward + cv_group_evidence_backward) on ragged label sets
-(gaps, negative and large label values, singleton groups, one group, n = 4096) — group rows 1e-5 relative
+(gaps, negative and large label values, singleton groups, one group, n = 4096, and n = 8192 / 10000 above the
+labels' LDS cache) — group rows 1e-5 relative
 (fp32 segmented sums vs fp64), member dict bit-exact, input gradients 1e-4 relative.  Fused step
 (HierarchicalVAETrainer, mode "group"): losses 1e-4 relative, VAE gradients by _check_grads, parameters
 after Adam median < 1e-5 / worst < 5e-3, as tests/test_gpu_parity.py."""
@@ -32,7 +33,9 @@ def _labels(n, kind, seed=0):
 
 @pytest.mark.parametrize("mode", ["GVAE", "MLVAE"])
 @pytest.mark.parametrize("n,d,kind", [(64, 8, "ragged"), (257, 32, "ragged"), (40, 8, "singletons"),
-                                      (16, 4, "one"), (4096, 8, "many")])
+                                      (16, 4, "one"), (4096, 8, "many"),
+                                      # above the LDS label cache (group_forward_kernel<true>): no batch cap
+                                      (8192, 8, "many"), (10000, 8, "ragged")])
 def test_group_evidence_module(mode, n, d, kind):
     from oracle import cpu_ref as R
     from src.models.vae import accumulate_group_evidence

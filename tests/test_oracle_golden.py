@@ -129,3 +129,44 @@ def test_bf16_conv_restatement():
             if not exact:  # the rounding is really in effect
                 y3 = f(h, w, b)
                 assert float((y3 - y).abs().max()) > 1e-4
+
+
+@pytest.mark.parametrize("sim_fn", ["cosine", "l2", "jeffrey", "mahalanobis", "modified_l2"])
+@pytest.mark.parametrize("ps", [False, True])
+def test_blockwise_contrastive_matches_reference_form(sim_fn, ps):
+    """oracle.cpu_ref.contrastive_loss_blockwise (the large-batch restatement used at N = 8192) against the
+    literal restatement of losses.py:98-126 at N = 96, value and gradient (fp64, 1e-12)."""
+    from oracle import cpu_ref as R
+
+    g = torch.Generator().manual_seed(3)
+    n, d = 96, 8
+    mu = torch.randn(n, d, generator=g, dtype=torch.float64)
+    lv = 0.3 * torch.randn(n, d, generator=g, dtype=torch.float64)
+    label = torch.randint(0, 4, (n,), generator=g)
+    label[5] = 99  # a singleton: an all -inf positive row (dropped by the finite-row mean when ps=False)
+    m1, l1 = mu.clone().requires_grad_(True), lv.clone().requires_grad_(True)
+    ref = R.contrastive_loss(m1, l1, label, sim_fn, 0.3, ps)
+    ref.backward()
+    m2, l2 = mu.clone().requires_grad_(True), lv.clone().requires_grad_(True)
+    got = R.contrastive_loss_blockwise(m2, l2, label, sim_fn, 0.3, ps, block=17)
+    assert abs(float(got) - float(ref)) <= 1e-12 * max(1.0, abs(float(ref)))
+    assert torch.allclose(m2.grad, m1.grad, rtol=1e-10, atol=1e-12)
+    if l1.grad is not None:
+        assert torch.allclose(l2.grad, l1.grad, rtol=1e-10, atol=1e-12)
+
+
+def test_l1out_closed_form_matches_broadcast():
+    """oracle.cpu_ref.l1out_closed against the literal [N,N,N] restatement (mi_estimator.py:170-191) at N = 48."""
+    from oracle import cpu_ref as R
+
+    g = torch.Generator().manual_seed(4)
+    M = R.to_torch(R.det_mlp(8, 16))
+    x = torch.randn(48, 8, generator=g, dtype=torch.float64, requires_grad=True)
+    y = torch.randn(48, 8, generator=g, dtype=torch.float64, requires_grad=True)
+    a = R.l1out(M, x, y)
+    b = R.l1out_closed(M, x, y)
+    assert abs(float(a) - float(b)) <= 1e-11 * max(1.0, abs(float(a)))
+    ga = torch.autograd.grad(a, (x, y))
+    gb = torch.autograd.grad(b, (x, y))
+    for u, v in zip(ga, gb):
+        assert torch.allclose(u, v, rtol=1e-9, atol=1e-12)
