@@ -535,7 +535,7 @@ def pipeline_pass(device, n=1024, hw=96, out=64, reps=50, cpu_budget_s=3.0):
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
                         "frac": round(gbs / PEAK_HBM_GBS, 4), "unit": "GB/s", "traffic": None,
                         "bytes_per_image": per_img}}
-    # HBM bytes per launch from the committed PMC passes of the same launch (scratch/pipe_pmc.py,
+    # HBM bytes per launch from the committed PMC passes of the same launch (tools/pipe_pmc.py,
     # profiles/pmc_traffic.py): taken at this shape only
     try:
         t = json.load(open(os.path.join(ROOT, "profiles", "pipeline_traffic.json")))["calls"]

@@ -1,6 +1,6 @@
 #!/bin/bash
 # MFMA busy cycles of one step-program call: SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE in one rocprofv3 pass
-# usage: scratch/pmc_mfma.sh <config> <call, e.g. 'enc[4]'>
+# usage: tools/pmc_mfma.sh <config> <call, e.g. 'enc[4]'>
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 cfg=$1; call=$2

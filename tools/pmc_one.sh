@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of one step-program call: scratch/pmc_one.sh CONFIG CALL TAG
+# SQ counters of one step-program call: tools/pmc_one.sh CONFIG CALL TAG
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 CFG=$1; C=$2; TAG=$3

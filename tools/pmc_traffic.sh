@@ -1,6 +1,6 @@
 #!/bin/bash
 # HBM traffic of one step-program call: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes
-# usage: scratch/pmc_traffic.sh <config> <full call label, e.g. 'enc[4]:cv_conv_backward_data'>
+# usage: tools/pmc_traffic.sh <config> <full call label, e.g. 'enc[4]:cv_conv_backward_data'>
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 cfg=$1; label=$2; call=${label%%:*}

@@ -16,7 +16,7 @@ if [ "$part" = trace ]; then
 fi
 if [ "$part" = pmc ]; then
   while read cfg label; do
-    bash scratch/pmc_traffic.sh $cfg "$label" > gpurun_out/pmct_${cfg}_$(echo ${label%%:*} | tr -d '[]').log 2>&1
+    bash tools/pmc_traffic.sh $cfg "$label" > gpurun_out/pmct_${cfg}_$(echo ${label%%:*} | tr -d '[]').log 2>&1
     echo "traffic $cfg $label done"
   done <<'LIST'
 mnist enc[3]:cv_conv_backward_data
@@ -31,7 +31,7 @@ mnist enc[5]:cv_conv_backward_weight_deferred
 celeba fwd[1]:cv_conv_forward
 celeba fwd[12]:cv_conv_forward
 LIST
-  bash scratch/pmc_mfma.sh mnist 'enc[3]' > gpurun_out/mfma_mnist.log 2>&1
+  bash tools/pmc_mfma.sh mnist 'enc[3]' > gpurun_out/mfma_mnist.log 2>&1
   echo "mfma done"
 fi
 if [ "$part" = sq ]; then
