@@ -209,14 +209,19 @@ def gemm_flops_of(label, G):
     if P is None:
         return None
     name, fn, args, _lane = P.calls[idx]
-    if name in ("cv_conv_forward", "cv_conv_backward_data", "cv_conv_backward_weight"):
+    # one contraction of the conv geometry: forward, backward-data or weight gradient (the `_kpack` entries carry
+    # the other weight packing too; cv_convt_output_loss is the last ConvTranspose2d with the loss fused in)
+    one = ("cv_conv_forward", "cv_conv_forward_kpack", "cv_convt_output_loss", "cv_conv_backward_data",
+           "cv_conv_backward_data_kpack", "cv_conv_backward_weight", "cv_conv_backward_weight_deferred")
+    two = ("cv_conv_backward_deferred", "cv_conv_backward_deferred_kpack")  # backward-data + weight gradient
+    if name in one or name in two:
         g = args[0]._obj
         k = g.kh * g.kw
         if g.transposed:
             macs = g.n * g.h_in * g.w_in * g.c_in * g.c_out * k
         else:
             macs = g.n * g.h_out * g.w_out * g.c_out * g.c_in * k
-        return 2.0 * macs
+        return 2.0 * macs * (2 if name in two else 1)
     if name in ("cv_linear_forward", "cv_linear_backward_data", "cv_linear_backward_weight"):
         g = args[0]._obj
         return 2.0 * g.n * g.in_features * g.out_features
@@ -226,16 +231,18 @@ def gemm_flops_of(label, G):
 def prefix_times(engine, G, labels, reps=20, rounds=3):
     """In-graph, in-step duration of the given calls: a graph of the step's calls up to and including call
     i, minus one up to call i-1, each replayed REPS times between HIP events on the launch stream (min of
-    ROUNDS).  Single-stream steps only (the default schedule); mutates the workspace (run after timing)."""
+    ROUNDS).  The step's main-lane calls only (data parallel: the side-lane weight-gradient calls and the
+    collectives between segments are left out, so a prefix is the single-stream chain the call runs in);
+    labels on a side lane are not timed.  Mutates the workspace (run after timing)."""
     from cvhip.plan import Program
 
-    flat = []  # (label, call) in step order
+    flat = []  # (label, call) in step order, main lane
     for pname, P in _programs(G):
         for i, c in enumerate(P.calls):
-            flat.append((f"{pname}[{i}]:{c[0]}", c))
-    if any(c[3] for _, c in flat):
-        return {}
+            if not c[3]:
+                flat.append((f"{pname}[{i}]:{c[0]}", c))
     pos = {lab: k for k, (lab, _) in enumerate(flat)}
+    labels = [lab for lab in labels if lab in pos]
 
     def t_prefix(k):
         if k < 0:
@@ -282,8 +289,8 @@ def roofline_of(config, G, instep, precision, engine=None):
     timing = "in-step HIP events on the call's stream (eager, event pairs per call)"
     if engine is not None:
         pt = prefix_times(engine, G, [lab for _, lab, _ in cands[:3]])
-        if pt:
-            cands = sorted(((pt[lab], lab, fl) for _, lab, fl in cands[:3]), reverse=True)
+        if pt:  # (the main-lane calls among the top three)
+            cands = sorted(((pt[lab], lab, fl) for _, lab, fl in cands[:3] if lab in pt), reverse=True)
             timing = "in-step, replayed step graph: t(prefix through the call) - t(prefix before it)"
     ms, label, fl = cands[0]
     best = (label, ms, fl)
@@ -465,7 +472,7 @@ def run_workload(name, cfg, steps, warmup, device, world, rank, detail=True, ker
         G = eng.graphs[B]
         instep = instep_pass(eng, G)
         res["instep"] = instep
-        res["roofline"] = roofline_of(name, G, instep, hp.get("precision", "fp32"), eng if world == 1 else None)
+        res["roofline"] = roofline_of(name, G, instep, hp.get("precision", "fp32"), eng)
         res["instep_sum_ms"] = sum(instep.values())
         if kernel_table and rank == 0:
             iso = isolated_pass(G)
@@ -595,7 +602,17 @@ def scaling_entry(cname, cfg, steps, device, world, rank, detail):
         e.update(r["comm"])
     if r.get("roofline") is not None:
         e["roofline"] = r["roofline"]
+    e["roofline_step"] = step_roofline(r["algorithmic_tflops"], world, cfg[7].get("precision", "fp32"))
     return e
+
+
+def step_roofline(alg_tflops, world, precision):
+    """Whole-step MFMA roofline of a key at N GPUs: the reference's algorithmic FLOP rate per GPU over the dense
+    peak of the compute dtype (the dominant call's own roofline is `roofline`)."""
+    peak = PEAK_BF16_TFLOPS if precision == "bf16" else PEAK_FP32_TFLOPS
+    per = alg_tflops / max(world, 1)
+    return {"bound": "mfma", "achieved_per_gpu": round(per, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(per / peak, 4), "n_gpus": world}
 
 
 def main():
@@ -697,7 +714,7 @@ def main():
             ccfg = CONFIGS[cname]
             assert ccfg[4] == bs, (cname, ccfg[4])
             scaling[key] = scaling_entry(cname, ccfg, min(args.steps, 100), device, world, rank,
-                                         detail=(world == 1 and not args.no_kernel_pass))
+                                         detail=not args.no_kernel_pass)
     if rank == 0:
         rec = {
             "metric": "training images/sec at bs=512; ELBO rel-err vs CPU ref",
@@ -716,6 +733,7 @@ def main():
             "algorithmic_tflops": round(res["algorithmic_tflops"], 3),
             "losses_finite": res["finite"],
             "roofline": res.get("roofline"),
+            "roofline_step": step_roofline(res["algorithmic_tflops"], world, hp.get("precision", "fp32")),
             "instep_sum_ms": round(res["instep_sum_ms"], 4) if "instep_sum_ms" in res else None,
         }
         if "comm" in res:

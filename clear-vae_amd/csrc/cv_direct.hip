@@ -11,12 +11,20 @@
 //   1. the small-grid rows the band reads (plus a zero halo = the convolution's padding) are loaded, transformed
 //      (BN+ReLU forward, or the BN backward of the layer below) and written to LDS once, channel-chunked
 //      [cs/32][pixel][32 + 4] so a fragment read of 16 consecutive blocks is bank-conflict free;
-//   2. the classes run one after another on one accumulator set: for class (dy, dx) and each of its taps (kh, kw)
+//   2. the classes run one after another, each on its own accumulators: for class (dy, dx) and each tap (kh, kw)
 //      the A fragment of block m is the LDS region pixel base(m) + toff(tap) — a uniform shift per tap, no
-//      address arithmetic per element — and the tap's weights [cb][cs] stream through a 2-stage LDS ring
-//      (k-contiguous `gather` packing [tap][cb][cs], one 16-byte load and one ds_write_b128 per thread);
-//   3. each class's epilogue writes its output pixels (bias, the STAT_FWD sums, or the STAT_BWD ReLU mask and
-//      BN-backward sums of the layer above, with the pre-BN values prefetched while the class computes).
+//      address arithmetic per element — and the tap's weights [cb][cs] (k-contiguous `gather` packing
+//      [tap][cb][cs]) stream by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) through a ring PRIVATE to
+//      each wave (its own 16 output channels, NSL slots, NSL - 1 stages ahead): a wave waits only for its own
+//      DMA with a counted vmcnt, so the stage loop has no workgroup barrier at all and the waves of a CU drift
+//      freely against each other (a per-stage barrier measured 0.76 us per stage against 0.43 of MFMA work).
+//      The DMA writes lane-linear, so the XOR swizzle of a column's 8 quads (quad q stored at q ^ ((col >> 1)
+//      & 7)) is applied on the source address; it keeps the B fragment reads conflict free without a pad;
+//   3. all classes' epilogues run after the last stage (bias, the STAT_FWD sums, or the STAT_BWD ReLU mask and
+//      BN-backward sums of the layer above, with the pre-BN values loaded before the first stage): no ordinary
+//      global load or store sits between two weight stages, so the counted vmcnt waits never drain the ring.
+//      The MFMA runs transposed (weights as the row operand), so a lane holds 4 consecutive channels of one
+//      output pixel and the epilogue moves float4s.
 // The contraction is the GEMM core's: the same k order within a tap (4 k per lane group, 16-k halves), taps in
 // (kh, kw) order, fp32 MFMA accumulation; only the order in which taps are summed differs from the per-class GEMM
 // (tap-major there too), so results agree with the core to fp32 rounding (tests/test_gpu_direct.py).
@@ -28,6 +36,8 @@
 // uniform shift (kh >> 1, kw >> 1) and 16 consecutive output pixels read 16 consecutive plane pixels (the
 // stride-2 walk of the big grid would put every second lane on the same LDS banks).  Its B operand is the
 // `scatter` packing [tap][cs][cb] (k = big-grid channel contiguous per output channel).
+#include <cstdio>
+
 #include "cv_gemm.hpp"
 
 namespace cv {
@@ -37,6 +47,45 @@ constexpr int CK = 32;     // channels per LDS chunk = K elements of one weight 
 constexpr int PP = CK + 4; // LDS pitch (floats) of a region pixel's chunk and of a weight column's chunk
 constexpr int MAXST = 64;  // stages (taps x channel chunks) per workgroup
 constexpr int RQ = 4;      // region float4 per thread per staging round
+#ifndef CV_DIRECT_NSL
+#define CV_DIRECT_NSL 4
+#endif
+constexpr int NSL = CV_DIRECT_NSL;  // weight ring slots per wave (stages in flight: NSL - 1 issued ahead)
+constexpr int RING = NSL * 4 * 16 * CK;  // ring floats per workgroup: 4 waves x NSL slots x 16 columns x CK
+
+#ifdef CV_STAMPS
+// instrumented builds only (make stamps): per-workgroup phase timeline [wg][8] u64 = {entry, constants staged,
+// region staged, stages done, epilogue stores done, exit, HW_ID, XCC_ID} (s_memrealtime, 100 MHz)
+static __device__ unsigned long long* g_dstamps;
+#define CV_DSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#else
+#define CV_DSTAMP(v)
+#endif
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+// wait until at most n of this wave's vector-memory operations are outstanding (n wave-uniform, 0..15)
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
 
 struct DArgs {
   Geo g;
@@ -74,12 +123,13 @@ __global__ __launch_bounds__(NT, 2) void direct_kernel(const DArgs P) {
   const int grp = blockIdx.x / P.nband, band = blockIdx.x - grp * P.nband;
   const int img0 = grp * P.ipw, by0 = band * P.br;
   const int n0 = blockIdx.y * CBT;
+  CV_DSTAMP(st0);
   // staged tensor's grid
   const int sh = SC ? g.hs : g.hb, sw = SC ? g.ws : g.wb;
 
   float* Rg = smem;                             // [nck][rpix][PP]
-  float* Bs = Rg + P.nck * P.rpix * PP;         // [2][CBT][PP]
-  float* cA = Bs + 2 * CBT * PP;                // A transform constants (SoA, ci each)
+  float* Bs = Rg + P.nck * P.rpix * PP;         // [wave][NSL][16][CK], quads swizzled
+  float* cA = Bs + RING;                        // A transform constants (SoA, ci each)
   float* cE = cA + fast::soa_arrays<XA>() * ci; // STAT_BWD: BnFwdC[co] of the output's BatchNorm
   float* red = cE + (EPI == CV_STAT_BWD ? 4 * co : 0);  // [WM][2][CBT]
 
@@ -137,7 +187,28 @@ __global__ __launch_bounds__(NT, 2) void direct_kernel(const DArgs P) {
       });
     }
   }
-  __syncthreads();
+  __syncthreads();  // (the ring doubled as bn scratch above)
+  CV_DSTAMP(st1);
+  // ---------------- weight stages: every wave streams ITS OWN 16 columns (n0 + wn * 16 + 0..15) through a private
+  // NSL-slot ring — no workgroup barrier between stages, each wave waits only for its own DMA (waves of one
+  // column group, WM = 2, fetch the same columns twice: L2 traffic, not HBM).  Slot j % NSL holds stage j as
+  // [16][CK], quad q of local column cl at q ^ ((cl >> 1) & 7); two 1 KB instructions (8 columns each) per stage.
+  constexpr int WPW = 2;
+  float* ring = Bs + wid * (NSL * 16 * CK);
+  auto issue_at = [&](int wofs, int j) {
+    float* slot = ring + (j % NSL) * 16 * CK;
+    const float* src = P.wk + wofs + (n0 + wn * 16) * ci;
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int cl = 8 * i + (lane >> 3), q = (lane & 7) ^ ((cl >> 1) & 7);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + cl * ci + 4 * q), (lds_void*)(slot + i * 8 * CK), 16,
+                                       0, 0);
+    }
+  };
+  {
+    const int pre = P.nst < NSL - 1 ? P.nst : NSL - 1;
+    for (int k = 0; k < pre; ++k) issue_at(P.wofs[k], k);
+  }
   fast::XC xc;
   if constexpr (XA != CV_XF_NONE) xc = fast::load_xc<XA>(cA, ci, 4 * (t % c4n));
   auto rstore = [&](const Rs& S, int u0) {
@@ -161,150 +232,166 @@ __global__ __launch_bounds__(NT, 2) void direct_kernel(const DArgs P) {
     if (more) S0 = S1;
   }
 
-  // ---------------- weight stages: [CBT][PP] per stage, 2-stage LDS ring, loads one stage ahead
-  constexpr int WQ = CBT * 8 / NT;  // float4 per thread per stage
-  f32x4 wr[WQ];
-  auto wload = [&](int j) {
-    const float* src = P.wk + P.wofs[j] + n0 * ci;
-#pragma unroll
-    for (int q = 0; q < WQ; ++q) {
-      const int idx = t + q * NT, col = idx >> 3, kq = idx & 7;
-      wr[q] = fast::g4(src + col * ci + 4 * kq);
-    }
-  };
-  auto wstore = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < WQ; ++q) {
-      const int idx = t + q * NT, col = idx >> 3, kq = idx & 7;
-      *reinterpret_cast<f32x4*>(Bs + buf * CBT * PP + col * PP + 4 * kq) = wr[q];
-    }
-  };
-  wload(0);
-  wstore(0);
-  if (P.nst > 1) wload(1);
-
-  // ---------------- per-lane rows: A fragment row (lane & 15) and the 4 epilogue rows of every fragment
+  // ---------------- per-lane units.  The MFMA runs transposed — weights as its row operand, the staged units as
+  // its column operand — so a lane's accumulator holds 4 CONSECUTIVE output channels of one unit: the epilogue
+  // moves float4s (stores, pre-BN loads), 4x fewer memory instructions than one channel per lane.
+  // Lane: unit m = f * 16 + (lane & 15) of fragment f, channels n0 + wn * 16 + 4 * (lane >> 4) + (0..3).
   const int fr = lane & 15, fk = 4 * (lane >> 4);
   const int blk = P.br * P.nbx;
   int abase[FMX];
-  int ob[FMX][4];    // output element offset of block row m's pixel (2by, 2bx), channel 0; -1: no such block
-  unsigned obf[FMX]; // per row r: bit 2r = row 2by+1 inside the image, bit 2r+1 = column 2bx+1 inside
+  int ob[FMX];        // output element offset of unit m's pixel (SCATTER: block pixel (2by, 2bx)), channel 0; -1: none
+  unsigned obf = 0u;  // fragment i: bit 2i = row 2by+1 inside the image, bit 2i+1 = column 2bx+1 inside
 #pragma unroll
   for (int i = 0; i < FMX; ++i) {
-    const int f = wm + WM * i;
-    {
-      const int m = f * 16 + fr;
-      int base = 0;
-      if (m < P.M) {
-        const int il = P.f_blk.div(m), rem = m - il * blk;
-        const int byl = P.f_nbx.div(rem), bx = rem - byl * P.nbx;
-        base = (il * P.r1 + byl) * P.c1 + bx;  // (GATHER: plane 0; the tap's plane is in its offset)
-      }
-      abase[i] = base * PP + fk;
-    }
-    obf[i] = 0u;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = f * 16 + 4 * (lane >> 4) + r;
-      int o = -1;
-      if (m < P.M) {
-        const int il = P.f_blk.div(m), rem = m - il * blk;
-        const int byl = P.f_nbx.div(rem), bx = rem - byl * P.nbx;
-        const int n = img0 + il, by = by0 + byl;
-        if (n < g.n && by < P.nby) {
-          if constexpr (SC) {
-            o = ((n * g.hb + 2 * by) * g.wb + 2 * bx) * co;
-            obf[i] |= ((2 * by + 1 < g.hb) ? 1u : 0u) << (2 * r);
-            obf[i] |= ((2 * bx + 1 < g.wb) ? 1u : 0u) << (2 * r + 1);
-          } else {
-            o = ((n * g.hs + by) * g.ws + bx) * co;
-          }
+    const int m = (wm + WM * i) * 16 + fr;
+    int base = 0, o = -1;
+    if (m < P.M) {
+      const int il = P.f_blk.div(m), rem = m - il * blk;
+      const int byl = P.f_nbx.div(rem), bx = rem - byl * P.nbx;
+      base = (il * P.r1 + byl) * P.c1 + bx;  // (GATHER: plane 0; the tap's plane is in its offset)
+      const int n = img0 + il, by = by0 + byl;
+      if (n < g.n && by < P.nby) {
+        if constexpr (SC) {
+          o = ((n * g.hb + 2 * by) * g.wb + 2 * bx) * co;
+          obf |= ((2 * by + 1 < g.hb) ? 1u : 0u) << (2 * i);
+          obf |= ((2 * bx + 1 < g.wb) ? 1u : 0u) << (2 * i + 1);
+        } else {
+          o = ((n * g.hs + by) * g.ws + bx) * co;
         }
       }
-      ob[i][r] = o;
     }
+    abase[i] = base * PP + fk;
+    ob[i] = o;
   }
-  const int col = n0 + wn * 16 + fr;  // this lane's output channel
-  const float bcol = P.bias ? P.bias[col] : 0.f;
-  __syncthreads();  // region and weight stage 0 visible
-
-  f32x4 acc[FMX];
-  float s1 = 0.f, s2 = 0.f;
-  float eyv[EPI == CV_STAT_BWD ? FMX : 1][4];
-  const float* Bw = Bs + (wn * 16 + fr) * PP + fk;
-  int j = 0;
-  for (int c = 0; c < P.ncls; ++c) {
+  const int ch = wn * 16 + fk;  // this lane's first output channel within the tile
+  f32x4 bias4 = fast::zero4();
+  if (P.bias) bias4 = fast::g4(P.bias + n0 + ch);
+  constexpr int NC = SC ? 4 : 1;  // classes
+  auto pix_ok = [&](int c, int i) -> bool {
     const int dy = SC ? c >> 1 : 0, dx = SC ? c & 1 : 0;
-    const int cofs = (SC ? (dy * g.wb + dx) * co : 0) + col;
-    auto pix_ok = [&](int i, int r) -> bool {
-      return ob[i][r] >= 0 && (!dy || ((obf[i] >> (2 * r)) & 1u)) && (!dx || ((obf[i] >> (2 * r + 1)) & 1u));
-    };
-    if constexpr (EPI == CV_STAT_BWD) {  // the class's pre-BN values, in flight while it computes
+    return ob[i] >= 0 && (!dy || ((obf >> (2 * i)) & 1u)) && (!dx || ((obf >> (2 * i + 1)) & 1u));
+  };
+  auto cofs = [&](int c) -> int { return (SC ? ((c >> 1) * g.wb + (c & 1)) * co : 0) + n0 + ch; };
+  f32x4 eyv[EPI == CV_STAT_BWD ? NC : 1][EPI == CV_STAT_BWD ? FMX : 1];
+  if constexpr (EPI == CV_STAT_BWD) {  // every class's pre-BN values, before the ring starts
 #pragma unroll
-      for (int i = 0; i < FMX; ++i)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) eyv[i][r] = P.ep.ey[pix_ok(i, r) ? ob[i][r] + cofs : 0];
+      for (int i = 0; i < FMX; ++i) eyv[c][i] = fast::g4(P.ep.ey + (pix_ok(c, i) ? ob[i] + cofs(c) : 0));
+  }
+  __syncthreads();  // region visible (and the ring's first NSL - 1 stages landed)
+  CV_DSTAMP(st2);
+
+  f32x4 acc[NC][FMX];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < FMX; ++i) acc[c][i] = fast::zero4();
+  const int bsw = (fr >> 1) & 7;
+  const float* Bw = ring + fr * CK;
+  // Software pipeline: while stage j's MFMAs run, stage j + 1's fragments are read from LDS (its DMA waited for
+  // first) and the stage tables' next entries are already in registers — the MFMAs never wait on an LDS or a
+  // scalar load.  (A fragment past the last unit reads region pixel 0 and is discarded by the epilogue: no
+  // per-MFMA branch, which would split every MFMA into its own exec-masked block.)
+  struct Frag {
+    f32x4 a[CK / 16][FMX], b[CK / 16];
+  };
+  auto frag = [&](int aofs, int j, Frag& F) {
+    const float* Ab = Rg + aofs;
+    const float* Bb = Bw + (j % NSL) * 16 * CK;
+#pragma unroll
+    for (int kc = 0; kc < CK / 16; ++kc) {
+#pragma unroll
+      for (int i = 0; i < FMX; ++i) F.a[kc][i] = fast::lds4(Ab + abase[i] + kc * 16);
+      F.b[kc] = fast::lds4(Bb + 4 * ((kc * 4 + (lane >> 4)) ^ bsw));
+    }
+  };
+  const int nst = P.nst, last = nst - 1;
+  Frag fa, fb;  // ping-pong fragment sets (the loop is unrolled by two so neither is ever copied)
+  frag(P.aofs[0], 0, fa);  // (stage 0 landed: the barrier above drained every DMA)
+  int ao_n = P.aofs[last < 1 ? last : 1];             // stage j + 1's region offset
+  int wo_n = P.wofs[last < NSL - 1 ? last : NSL - 1];  // stage j + NSL - 1's weight offset
+  // one stage: stage j's MFMAs on `cur` while stage j + 1's fragments load into `nxt`
+  auto step = [&](int j, f32x4* ac, const Frag& cur, Frag& nxt) {
+    // slot (j - 1) % NSL is free: stage j - 1's fragments were read (and returned) during stage j - 2
+    if (j + NSL - 1 < nst) issue_at(wo_n, j + NSL - 1);
+    wo_n = P.wofs[j + NSL < last ? j + NSL : last];
+    if (j < last) {
+      const int ahead = last - 1 - j < NSL - 2 ? last - 1 - j : NSL - 2;
+      wait_vm(ahead * WPW);  // stage j + 1 landed (this wave's own DMA; stages after it stay in flight)
+      frag(ao_n, j + 1, nxt);
+      ao_n = P.aofs[j + 2 < last ? j + 2 : last];
     }
 #pragma unroll
-    for (int i = 0; i < FMX; ++i) acc[i] = fast::zero4();
-    const int jend = P.cend[c];
-    for (; j < jend; ++j) {
-      const int buf = j & 1;
-      if (j + 1 < P.nst) wstore(buf ^ 1);  // stage j + 1, loaded during stage j - 1
-      if (j + 2 < P.nst) wload(j + 2);
-      const float* Ab = Rg + P.aofs[j];
-      const float* Bb = Bw + buf * CBT * PP;
+    for (int kc = 0; kc < CK / 16; ++kc)
 #pragma unroll
-      for (int kc = 0; kc < CK / 16; ++kc) {
-        f32x4 av[FMX];
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int i = 0; i < FMX; ++i)
-          if (wm + WM * i < P.nfrag) av[i] = fast::lds4(Ab + abase[i] + kc * 16);
-        const f32x4 bv = fast::lds4(Bb + kc * 16);
+          ac[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.b[kc][s], cur.a[kc][i][s], ac[i], 0, 0, 0);
+  };
+  int j = 0;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < FMX; ++i)
-            if (wm + WM * i < P.nfrag) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][s], bv[s], acc[i], 0, 0, 0);
-      }
-      __syncthreads();
+  for (int c = 0; c < NC; ++c) {
+    const int jend = P.cend[c];
+    for (; j + 1 < jend; j += 2) {
+      step(j, acc[c], fa, fb);
+      step(j + 1, acc[c], fb, fa);
     }
-    // epilogue of class (dy, dx)
+    if (j < jend) {  // odd tail: the next stage's fragments land in fb; one copy per class
+      step(j, acc[c], fa, fb);
+      fa = fb;
+      ++j;
+    }
+  }
+  CV_DSTAMP(st3);
+  // epilogues of every class (dy, dx): float4 per (unit, 4 channels)
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  BnFwdC kc4[EPI == CV_STAT_BWD ? 4 : 1];
+  if constexpr (EPI == CV_STAT_BWD) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kc4[r] = reinterpret_cast<const BnFwdC*>(cE)[n0 + ch + r];
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
 #pragma unroll
     for (int i = 0; i < FMX; ++i) {
-      if (wm + WM * i >= P.nfrag) continue;
+      if (!pix_ok(c, i)) continue;
+      f32x4 v = acc[c][i];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (!pix_ok(i, r)) continue;
-        const int off = ob[i][r] + cofs;
-        float v = acc[i][r] + bcol;
+        v[r] += bias4[r];
         if constexpr (EPI == CV_STAT_BWD) {
-          const float yv = eyv[i][r];
-          const BnFwdC k = reinterpret_cast<const BnFwdC*>(cE)[col];
-          if (P.ep.erelu && bn_out(yv, k) <= 0.f) v = 0.f;
-          P.out[off] = v;
-          s1 += v;
-          s2 += v * ((yv - k.mu) * k.istd);
-        } else {
-          P.out[off] = v;
-          if constexpr (EPI == CV_STAT_FWD) {
-            s1 += v;
-            s2 += v * v;
-          }
+          const float yv = eyv[c][i][r];
+          if (P.ep.erelu && bn_out(yv, kc4[r]) <= 0.f) v[r] = 0.f;
+          s1[r] += v[r];
+          s2[r] += v[r] * ((yv - kc4[r].mu) * kc4[r].istd);
+        } else if constexpr (EPI == CV_STAT_FWD) {
+          s1[r] += v[r];
+          s2[r] += v[r] * v[r];
         }
       }
+      *reinterpret_cast<f32x4*>(P.out + ob[i] + cofs(c)) = v;
     }
   }
 
-  // ---------------- statistics: lanes of one column (l, l+16, l+32, l+48), the WM row waves, one fp64 replica
+  CV_DSTAMP(st4);
+  // ---------------- statistics: the 16 lanes of one channel quad (xor 1..8), the WM row waves, one fp64 replica
   if constexpr (EPI != CV_STAT_NONE) {
-    s1 += __shfl_xor(s1, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    s2 += __shfl_xor(s2, 16, 64);
-    s2 += __shfl_xor(s2, 32, 64);
-    if (lane < 16) {
-      red[(wm * 2 + 0) * CBT + wn * 16 + lane] = s1;
-      red[(wm * 2 + 1) * CBT + wn * 16 + lane] = s2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[r] += __shfl_xor(s1[r], o, 64);
+        s2[r] += __shfl_xor(s2[r], o, 64);
+      }
+    }
+    if (fr == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[(wm * 2 + 0) * CBT + ch + r] = s1[r];
+        red[(wm * 2 + 1) * CBT + ch + r] = s2[r];
+      }
     }
     __syncthreads();
     if (t < CBT) {
@@ -323,6 +410,15 @@ __global__ __launch_bounds__(NT, 2) void direct_kernel(const DArgs P) {
     bn_finalize<NT>(P.ep.ebn, P.ep.stat_out, EPI == CV_STAT_BWD, reinterpret_cast<double*>(smem),
                     reinterpret_cast<int*>(smem + 8 * NT + 4));
   }
+#ifdef CV_STAMPS
+  if (t == 0 && g_dstamps) {
+    const unsigned long long st5 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o = g_dstamps + (size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 8;
+    o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st4; o[5] = st5;
+    o[6] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    o[7] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+  }
+#endif
 }
 
 // ---------------------------------------------------------------- host side
@@ -337,7 +433,7 @@ static int enabled() {  // CV_DIRECT=0: the per-class GEMM core instead (A/B bas
 
 static size_t lds_floats(const DArgs& a, int XA, int EPI, int CBT) {
   const size_t region = (size_t)a.nck * a.rpix * PP;
-  size_t n = region + 2 * (size_t)CBT * PP + (size_t)xf_floats(XA, a.ci) + (EPI == CV_STAT_BWD ? 4 * a.co : 0) +
+  size_t n = region + (size_t)RING + (size_t)xf_floats(XA, a.ci) + (EPI == CV_STAT_BWD ? 4 * a.co : 0) +
              2 * 4 * (size_t)CBT;
   const size_t fin = 8 * NT + 8;  // bn_finalize scratch (4 * NT doubles) + flag, at the start of the region
   return n > fin ? n : fin;
@@ -345,6 +441,7 @@ static size_t lds_floats(const DArgs& a, int XA, int EPI, int CBT) {
 
 template <int OP, int XA, int EPI, int CBT>
 static const void* pick(int fmx) {
+  if (fmx <= 1) return (const void*)direct_kernel<OP, XA, EPI, CBT, 1>;
   if (fmx <= 2) return (const void*)direct_kernel<OP, XA, EPI, CBT, 2>;
   return (const void*)direct_kernel<OP, XA, EPI, CBT, 4>;
 }
@@ -366,6 +463,7 @@ static const void* pick_kernel(int xa, int epi, int cbt, int fmx) {
 }
 
 static long g_minwg = -1;  // fewest workgroups worth a direct launch (cv_debug_direct_minwg, CV_DIRECT_MINWG)
+static int g_gather_rule = 1;  // GATHER only where it beats the GEMM core (0: every geometry; cv_debug_direct_gather_rule)
 
 // build the launch (tile choice, class taps, stage tables); false when the geometry is not served
 static bool plan(const Geo& g, int op, DArgs& a, int& cbt, long& nwg) {
@@ -415,16 +513,26 @@ static bool plan(const Geo& g, int op, DArgs& a, int& cbt, long& nwg) {
   a.c1 = a.nbx + (oxmax - oxmin);
   const int halo = oymax - oymin;  // extra region rows per band (GATHER: per plane)
   // tile: ~64 units per workgroup (a band of rows of one image, or several whole small images), halved while the
-  // grid has fewer than two workgroups per CU or the region exceeds ~64 KB of LDS, keeping >= 16 rows per row wave
+  // grid has fewer than two workgroups per CU or region + ring exceed ~80 KB of LDS, keeping >= 16 rows per row wave
   const int nbimg = a.nby * a.nbx;
   const long ntile_n = a.co / cbt;
-  if (nbimg >= 32) {
+  // units per workgroup (CV_DIRECT_UNITS, default 64) and the grid below which tiles are halved
+  // (CV_DIRECT_MINGRID, default 512 = two workgroups per CU); 64-channel tiles (one row wave) keep <= 64 units
+  static int U = -1, MG = -1;
+  if (U < 0) {
+    const char* e = getenv("CV_DIRECT_UNITS");
+    const char* f = getenv("CV_DIRECT_MINGRID");
+    U = e ? atoi(e) : 64;
+    MG = f ? atoi(f) : 512;
+  }
+  const int units = cbt == 64 && U > 64 ? 64 : U;
+  if (2 * nbimg >= units) {
     a.ipw = 1;
-    a.br = 64 / a.nbx < 1 ? 1 : 64 / a.nbx;
+    a.br = units / a.nbx < 1 ? 1 : units / a.nbx;
     if (a.br > a.nby) a.br = a.nby;
   } else {
     a.br = a.nby;
-    a.ipw = 64 / nbimg < 1 ? 1 : 64 / nbimg;
+    a.ipw = units / nbimg < 1 ? 1 : units / nbimg;
   }
   auto rows_of = [&](int br) -> int { return sc ? br + halo : 4 * (br + halo); };
   auto grid_of = [&]() -> long { return (long)cdiv(g.n, a.ipw) * cdiv(a.nby, a.br) * ntile_n; };
@@ -435,14 +543,21 @@ static bool plan(const Geo& g, int op, DArgs& a, int& cbt, long& nwg) {
     if (a.ipw == 1 && a.br > 1 && (a.br + 1) / 2 * a.nbx >= mmin) { a.br = (a.br + 1) / 2; return true; }
     return false;
   };
-  while ((grid_of() < 512 || region_floats() > 16 * 1024) && halve()) {
+  // LDS: region + the weight ring within ~80 KB (two workgroups per CU) where the tile can shrink that far; past
+  // that one workgroup per CU (the caller's LDS check, 160 KB)
+  const long ring = RING;
+  while ((grid_of() < MG || region_floats() > 20 * 1024 - ring) && halve()) {
   }
-  if (region_floats() > 20 * 1024) return false;
+  if (region_floats() > 36 * 1024 - ring) return false;
   if (g_minwg < 0) {
     const char* e = getenv("CV_DIRECT_MINWG");
     g_minwg = e ? atol(e) : 256;
   }
   if (grid_of() < g_minwg) return false;
+  // GATHER pays its region (four parity planes of the big grid) per 16-64 output pixels: measured slower than the
+  // GEMM core unless one resident round of workgroups covers the call and a tile holds >= 32 pixels (MNIST
+  // conv2 / convT2 backward-data win; the 16-pixel tiles and VAE64's multi-round grids lose)
+  if (!sc && g_gather_rule && (grid_of() > 512 || (long)a.ipw * a.br * a.nbx < 32)) return false;
   a.br = cdiv(a.nby, cdiv(a.nby, a.br));  // even bands
   a.nband = cdiv(a.nby, a.br);
   a.pr = a.br + halo;
@@ -479,6 +594,12 @@ static bool plan(const Geo& g, int op, DArgs& a, int& cbt, long& nwg) {
 }
 
 }  // namespace direct
+
+#ifdef CV_STAMPS
+extern "C" int cv_debug_set_stamps_direct(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(cv::direct::g_dstamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 static int g_direct_launches = 0;  // test hook cv_debug_direct_count
 
@@ -518,10 +639,19 @@ static int direct_run(int op, const Geo& g, const cv_operand* in, const float* w
   const int wm = cbt == 32 ? 2 : 1;
   const int fmx = cdiv(a.nfrag, wm);
   if (fmx > 4) return -1;
+  {
+    static int log = -1;
+    if (log < 0) log = getenv("CV_DIRECT_LOG") ? 1 : 0;
+    if (log)
+      fprintf(stderr, "direct %s n=%d big=%dx%dx%d small=%dx%dx%d k=%d ci=%d co=%d cbt=%d ipw=%d br=%d nby=%d M=%d "
+              "nfrag=%d fmx=%d nst=%d wgs=%ld region_kb=%.1f\n", op == OP_SCATTER ? "scatter" : "gather", g.n, g.hb,
+              g.wb, g.cb, g.hs, g.ws, g.cs, g.kh, a.ci, a.co, cbt, a.ipw, a.br, a.nby, a.M, a.nfrag, fmx, a.nst, nwg,
+              a.nck * a.rpix * PP * 4.0 / 1024);
+  }
   const void* kern = op == OP_SCATTER ? pick_kernel<OP_SCATTER>(in->xf, epi, cbt, fmx)
                                       : pick_kernel<OP_GATHER>(in->xf, epi, cbt, fmx);
   const size_t lds = lds_floats(a, in->xf, epi, cbt) * sizeof(float);
-  if (lds > 96 * 1024) return -1;
+  if (lds > 160 * 1024) return -1;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
     (void)hipGetLastError();
@@ -553,6 +683,12 @@ int direct_gather(const Geo& g, const cv_operand* in, const float* wk, const flo
 extern "C" int cv_debug_direct_minwg(int minwg) {
   const int prev = (int)cv::direct::g_minwg;
   cv::direct::g_minwg = minwg;
+  return prev;
+}
+
+extern "C" int cv_debug_direct_gather_rule(int on) {
+  const int prev = cv::direct::g_gather_rule;
+  cv::direct::g_gather_rule = on;
   return prev;
 }
 

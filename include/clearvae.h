@@ -538,6 +538,10 @@ int cv_debug_direct_count(int reset);
 /* test hook: the fewest workgroups for which a stride-2 conv takes the direct kernel (default 256; smaller
  * grids run the GEMM core); returns the previous setting (-1: not yet initialised) */
 int cv_debug_direct_minwg(int minwg);
+/* test hook: 1 (default) serves a stride-2 GATHER by the direct kernel only where it measured faster than the GEMM
+ * core (one resident round of workgroups, >= 32 output pixels per tile); 0 serves every geometry it can plan
+ * (kernel tests); returns the previous setting */
+int cv_debug_direct_gather_rule(int on);
 
 /* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
  * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least

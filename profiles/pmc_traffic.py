@@ -15,7 +15,8 @@ kernel (the warmup steps dispatch the same kernel for other layers first).
 
 (merges into out.json, keyed by the bench's full call label "program[index]:c_function", so a stale entry
 from an older program layout is never matched).  `auto`: the kernel of the trace's last dispatch — in
---only-call mode the last --reps dispatches are the call's own launches.
+--only-call mode the last --reps dispatches are the call's own launches.  `call`: every kernel the call
+launches, summed per repetition (the unit the bench's roofline prices).
 """
 
 import csv
@@ -36,8 +37,46 @@ def per_dispatch(path_glob, counter, kernel_sub):
     return [vals[k] for k in sorted(vals)]
 
 
+def per_call(path_glob, counter, reps):
+    """`call` mode: a call that launches K kernels per repetition (e.g. the direct backward-data + the deferred
+    weight gradient of cv_conv_backward_deferred_kpack) — the period K of the last dispatches' kernel names,
+    the counter summed over each repetition's K dispatches; (per-repetition sums, kernel names of one period)."""
+    vals, names = {}, {}
+    for path in glob.glob(path_glob, recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name") != counter:
+                continue
+            d = int(r["Dispatch_Id"])
+            vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
+            names[d] = r["Kernel_Name"]
+    ids = sorted(vals)
+    seq = [names[i] for i in ids]
+    for k in range(1, 9):
+        tail = seq[-k * reps:]
+        if len(tail) == k * reps and all(tail[i] == tail[i % k] for i in range(len(tail))):
+            break
+    else:
+        raise SystemExit("no periodic tail of call dispatches")
+    v = [vals[i] for i in ids[-k * reps:]]
+    return [sum(v[r * k:(r + 1) * k]) for r in range(reps)], seq[-k:]
+
+
 def main():
     d, call, ksub, reps, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    if ksub == "call":
+        fetch, kn = per_call(f"{d}/fetch/**/*counter_collection.csv", "FETCH_SIZE", reps)
+        write, _ = per_call(f"{d}/write/**/*counter_collection.csv", "WRITE_SIZE", reps)
+        f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+        rec = {"kernels": kn, "dispatches_per_call": len(kn), "fetch_size_kib_median": f_kib,
+               "write_size_kib_median": w_kib, "traffic_bytes": 2 * f_kib * 1024 + w_kib * 1024}
+        try:
+            db = json.load(open(out))
+        except (OSError, ValueError):
+            db = {"note": "per launch: traffic = 2*FETCH_SIZE (gfx950 16B-load correction) + WRITE_SIZE", "calls": {}}
+        db["calls"][call] = rec
+        json.dump(db, open(out, "w"), indent=1)
+        print(json.dumps({call: rec}))
+        return
     if ksub == "auto":
         last = (-1, None)
         for path in glob.glob(f"{d}/fetch/**/*counter_collection.csv", recursive=True):

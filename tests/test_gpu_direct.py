@@ -58,13 +58,16 @@ def _ids(v):
 
 @pytest.fixture(autouse=True)
 def _any_grid():
-    """The kernel-level cases run the direct kernel at any grid size (the product falls back to the GEMM core
-    below 256 workgroups, cv_debug_direct_minwg); restored afterwards."""
+    """The kernel-level cases run the direct kernel at any grid size and any GATHER tile (the product falls back
+    to the GEMM core below 256 workgroups, cv_debug_direct_minwg, and for the GATHER geometries where the core
+    measured faster, cv_debug_direct_gather_rule); restored afterwards."""
     from cvhip import _lib
 
     prev = _lib.lib().cv_debug_direct_minwg(1)
+    prev_rule = _lib.lib().cv_debug_direct_gather_rule(0)
     yield
     _lib.lib().cv_debug_direct_minwg(prev)  # (-1: re-read CV_DIRECT_MINWG / the default)
+    _lib.lib().cv_debug_direct_gather_rule(prev_rule)
 
 
 def _case(geom, direction, with_xf, seed):
@@ -194,3 +197,23 @@ def test_direct_conv_fallback(case):
     assert d[2] == 0, "the direct kernel does not serve this call"
     assert rel(d[0], ref) < TOL
     assert rel(d[1][0], want[0]) < 1e-5 and rel(d[1][1], want[1]) < 1e-5
+
+
+# the production choice for GATHER (cv_debug_direct_gather_rule 1): the MNIST bench's conv2 forward / convT2
+# backward-data (49-pixel tiles, 512 workgroups) take the direct kernel; MNIST conv3 forward (16-pixel tiles) and
+# the C3 shard's conv2 forward (1024 workgroups) run the GEMM core
+GATHER_RULE = [((_with_n("mnist_conv2", 512), "fwd"), 1), ((_with_n("mnist_convT2", 512), "bwd"), 1),
+               ((_with_n("mnist_conv3", 512), "fwd"), 0), ((_with_n("v64_conv2", 256), "fwd"), 0)]
+
+
+@pytest.mark.parametrize("case,served", GATHER_RULE, ids=lambda v: _ids(v) if isinstance(v, tuple) else str(v))
+def test_direct_gather_rule(case, served):
+    from cvhip import _lib
+
+    _lib.lib().cv_debug_direct_minwg(-1)
+    _lib.lib().cv_debug_direct_gather_rule(1)
+    geom, direction = case
+    outs, ref, want = _case(geom, direction, True, 9)
+    d = outs["direct"]
+    assert d[2] == served, (d[2], served)
+    assert rel(d[0], ref) < TOL

@@ -8,3 +8,4 @@ d=gpurun_out/mfma_${cfg}_${call//[\[\]]/_}
 rm -rf "$d"
 timeout -s KILL 150 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$d" -o run -- \
   python bench.py --config "$cfg" --only-call "$call" --reps 50 --warmup 5 --no-cpu-baseline --no-kernel-pass
+python profiles/pmc_mfma.py "$d" "$cfg $call" 50 | tee -a gpurun_out/mfma_util.jsonl

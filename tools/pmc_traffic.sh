@@ -11,4 +11,4 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$d/fetch"
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$d/write" -o run -- \
   python bench.py --config "$cfg" --only-call "$call" --reps 50 --warmup 5 --no-cpu-baseline --no-kernel-pass
 [ -f "gpurun_out/${cfg}_traffic.json" ] || { [ -f "profiles/${cfg}_traffic.json" ] && cp "profiles/${cfg}_traffic.json" gpurun_out/; } || true
-python profiles/pmc_traffic.py "$d" "$label" auto 50 "gpurun_out/${cfg}_traffic.json"
+python profiles/pmc_traffic.py "$d" "$label" call 50 "gpurun_out/${cfg}_traffic.json"
