@@ -104,6 +104,8 @@ struct DArgs {
   int rpix, nck;         // region pixels per chunk, channel chunks (ci / 32)
   int nst, ncls;         // weight stages (the classes' taps x channel chunks), classes (4 or 1)
   int cend[4];           // one past each class's last stage
+  int dbg;               // stamps builds only (CV_DIRECT_DBG): 1 = no weight DMA in the loop, 2 = no MFMA, 4 = no
+                         // fragment reads — timing ablations, results invalid
   int wofs[MAXST];       // stage -> weight offset tap * co * ci + chunk * 32
   int aofs[MAXST];       // stage -> LDS float offset of its A operand: (chunk * rpix + toff(tap)) * PP
   FDiv f_nbx, f_blk, f_rpi, f_rc, f_c4, f_pl;  // nbx, br * nbx, r1 * c1, c1, ci / 4, pr * c1
@@ -274,6 +276,8 @@ __global__ __launch_bounds__(NT, 2) void direct_kernel(const DArgs P) {
   auto cofs = [&](int c) -> int { return (SC ? ((c >> 1) * g.wb + (c & 1)) * co : 0) + n0 + ch; };
   f32x4 eyv[EPI == CV_STAT_BWD ? NC : 1][EPI == CV_STAT_BWD ? FMX : 1];
   if constexpr (EPI == CV_STAT_BWD) {  // every class's pre-BN values, before the ring starts
+    // (loaded inside the stage loop instead, under its counted waits, they measured slower: MNIST conv2
+    // backward-data 34.4 -> 35.4 us, VAE64 37-47 % of the STAT_BWD calls +1-5 %)
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
@@ -312,23 +316,30 @@ __global__ __launch_bounds__(NT, 2) void direct_kernel(const DArgs P) {
   int ao_n = P.aofs[last < 1 ? last : 1];             // stage j + 1's region offset
   int wo_n = P.wofs[last < NSL - 1 ? last : NSL - 1];  // stage j + NSL - 1's weight offset
   // one stage: stage j's MFMAs on `cur` while stage j + 1's fragments load into `nxt`
+#ifdef CV_STAMPS
+  const int dbg = P.dbg;
+#else
+  constexpr int dbg = 0;
+#endif
   auto step = [&](int j, f32x4* ac, const Frag& cur, Frag& nxt) {
     // slot (j - 1) % NSL is free: stage j - 1's fragments were read (and returned) during stage j - 2
-    if (j + NSL - 1 < nst) issue_at(wo_n, j + NSL - 1);
+    if (!(dbg & 1) && j + NSL - 1 < nst) issue_at(wo_n, j + NSL - 1);
     wo_n = P.wofs[j + NSL < last ? j + NSL : last];
     if (j < last) {
       const int ahead = last - 1 - j < NSL - 2 ? last - 1 - j : NSL - 2;
-      wait_vm(ahead * WPW);  // stage j + 1 landed (this wave's own DMA; stages after it stay in flight)
-      frag(ao_n, j + 1, nxt);
+      if (!(dbg & 1)) wait_vm(ahead * WPW);  // stage j + 1 landed (this wave's own DMA; later stages in flight)
+      if (!(dbg & 4)) frag(ao_n, j + 1, nxt);
       ao_n = P.aofs[j + 2 < last ? j + 2 : last];
     }
+    if (!(dbg & 2)) {
 #pragma unroll
-    for (int kc = 0; kc < CK / 16; ++kc)
+      for (int kc = 0; kc < CK / 16; ++kc)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < FMX; ++i)
-          ac[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.b[kc][s], cur.a[kc][i][s], ac[i], 0, 0, 0);
+          for (int i = 0; i < FMX; ++i)
+            ac[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.b[kc][s], cur.a[kc][i][s], ac[i], 0, 0, 0);
+    }
   };
   int j = 0;
 #pragma unroll
@@ -625,6 +636,12 @@ static int direct_run(int op, const Geo& g, const cv_operand* in, const float* w
   int cbt = 32;
   long nwg = 0;
   if (!plan(g, op, a, cbt, nwg)) return -1;
+#ifdef CV_STAMPS
+  {
+    const char* e = getenv("CV_DIRECT_DBG");
+    a.dbg = e ? atoi(e) : 0;
+  }
+#endif
   a.a = *in;
   a.wk = wk;
   a.bias = bias;
