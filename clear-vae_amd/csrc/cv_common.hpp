@@ -90,6 +90,11 @@ int direct_scatter(const Geo& g, const cv_operand* in, const float* wk, const fl
                    const cv_epilogue* ep, hipStream_t st, int mma);
 // the same for a stride-2 GATHER (Conv2d forward / ConvTranspose2d backward-data); wk = the `scatter` packing
 // [tap][cs][cb]
+// dual launch (cv_dual.hip): between dual_begin and dual_end this thread's next direct backward-data launch and
+// next GEMM-core weight-gradient launch are captured; dual_end issues them as one grid when the pair is served,
+// else back to back (issue = false: drops them, after an error)
+void dual_begin();
+int dual_end(hipStream_t st, bool issue);
 int direct_gather(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,
                   const cv_epilogue* ep, hipStream_t st, int mma);
 
@@ -268,8 +273,11 @@ __device__ __forceinline__ void bn_fold(const cv_bn& b, bool with_g, double* scr
 // Hand-off (cdna_hip_programming.md, Guideline 16): every wave drains its atomics (vmcnt(0)) before
 // the barrier, one lane adds to the ticket (agent scope), the electee acquires before its loads.
 // scratch: >= 4*NT doubles of LDS that are no longer live; flag: one int of LDS.
+// bn_finalize_at: the launch's workgroups counted as `nblk` with this one as `me` (a launch that runs another
+// kernel's workgroups beside these, cv_dual.hip, counts only its own role's).
 template <int NT>
-__device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, bool bwd, double* scratch, int* flag) {
+__device__ __forceinline__ void bn_finalize_at(cv_bn b, const double* produced, bool bwd, double* scratch, int* flag,
+                                               unsigned me, unsigned nblk) {
   float* out = bwd ? b.cbwd : b.cfwd;
 #ifdef CV_NO_FINALIZE  // A/B build: no producer-side finalisation (every consumer folds the replicas)
   return;
@@ -280,8 +288,6 @@ __device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, boo
   if (threadIdx.x == 0) {
     // two-level arrival count: <= 64 groups of gsz consecutive workgroups; the last of a group
     // arrives at ticket[dir], the last group elects the finalising workgroup
-    const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
-    const unsigned me = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     const unsigned gsz = (nblk + 63) / 64, ngrp = (nblk + gsz - 1) / gsz, grp = me / gsz;
     const unsigned gcnt = (grp + 1 == ngrp) ? nblk - grp * gsz : gsz;
     unsigned* gctr = b.ticket + 2 + (bwd ? 64 : 0) + grp;
@@ -318,6 +324,12 @@ __device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, boo
       out[4 * C + f] = k.c2;
     });
   }
+}
+
+template <int NT>
+__device__ __forceinline__ void bn_finalize(cv_bn b, const double* produced, bool bwd, double* scratch, int* flag) {
+  bn_finalize_at<NT>(b, produced, bwd, scratch, flag, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                     gridDim.x * gridDim.y * gridDim.z);
 }
 
 // (x - mu) first: the subtraction is exact for x near mu, so the sign test of a near-zero BN output

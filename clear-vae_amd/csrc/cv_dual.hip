@@ -1,0 +1,164 @@
+// Dual launch: a layer's stride-2 backward-data (the direct kernel, cv_direct.hpp) and its weight gradient (the
+// GEMM core's WGRAD tile, cv_gemm.hpp) as ONE grid whose workgroups alternate between the two.
+//
+// Why: both read only what earlier calls produced (the layer's output gradient, its input), so
+// they may run at the same time; and they are complementary — the direct kernel's workgroups spend their first
+// and last thirds on HBM bursts (staging its region, writing its output) around an MFMA-bound stage loop, the
+// WGRAD tiles are latency-bound K loops.  Run back to back each leaves most of the chip idle most of the time;
+// run side by side as two free-running streams they took 36-44 us instead of 51-62 us (MNIST conv2 / conv3 /
+// convT1, tools/overlap_probe.py), but a second stream costs ~10 us per cross-stream edge in the replayed step
+// graph, more than the overlap buys.  One grid has no edge: workgroup v < 2 min(nd, ng) is direct workgroup v/2
+// when v is even and WGRAD workgroup v/2 when odd (the dispatcher hands every CU some of each), the rest go to the
+// role with more workgroups.  Each role sees its own block coordinates and workgroup count (the direct kernel's
+// BatchNorm finalisation counts its own workgroups, bn_finalize_at), and the grid's LDS and registers are the
+// larger of the two.  Served pairs are the instantiations below; any other pair is launched back to back.
+// Measured: the one-grid form recovers only part of the free-running streams' overlap (MNIST conv2 pair
+// 62.9 -> 58.7 us, convT2 63.3 -> 58.3 us in-step) — the roles share each CU's LDS and register budget at the
+// larger of the two — and is used only where the direct grid is a single resident round.
+#include "cv_direct.hpp"
+
+namespace cv {
+namespace fast {
+thread_local GemmCap* g_gemm_cap = nullptr;
+}  // namespace fast
+namespace direct {
+thread_local DirectCap* g_direct_cap = nullptr;
+}  // namespace direct
+
+namespace dual {
+
+struct DualMap {
+  int nd, dgx, dgy;       // direct workgroups and their grid
+  int ng, ggx, ggy, ggz;  // WGRAD workgroups and their grid
+};
+
+template <int DOP, int DXA, int DEPI, int DCBT, int DFMX, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
+__global__ __launch_bounds__(NT, 2) void dual_kernel(const direct::DArgs PD, const Args PG, const DualMap m) {
+  const int v = blockIdx.x;
+  const int k = m.nd < m.ng ? m.nd : m.ng;
+  int role, idx;
+  if (v < 2 * k) {
+    role = v & 1;
+    idx = v >> 1;
+  } else {
+    role = m.nd > m.ng ? 0 : 1;
+    idx = k + (v - 2 * k);
+  }
+  if (role == 0) {
+    direct::direct_body<DOP, DXA, DEPI, DCBT, DFMX>(PD, idx % m.dgx, idx / m.dgx, m.dgx, m.dgy);
+  } else {
+    const int r = idx / m.ggx;
+    fast::gemm_body<OP_WGRAD, BM, BN, XA, XB, EPI, D, MT>(PG, idx % m.ggx, r % m.ggy, r / m.ggy, m.ggx, m.ggy, m.ggz);
+  }
+}
+
+struct Ent {
+  int dk[5];  // direct OP, XA, EPI, CBT, FMX
+  int gk[7];  // WGRAD BM, BN, XA, XB, EPI, D, MT
+  const void* fn;
+};
+#define CV_DUAL(a, b, c, d, e, f, g, h, i, j, k, l) \
+  Ent{{a, b, c, d, e}, {f, g, h, i, j, k, l}, (const void*)dual_kernel<a, b, c, d, e, f, g, h, i, j, k, l>}
+// the pairs of the bench configurations' backward passes (fp32, 64-row WGRAD tiles: both roles fit two
+// workgroups per CU): MNIST / VAE64 conv2 (backward-data SCATTER with the BN-backward transform and STAT_BWD +
+// the weight gradient of the BN+ReLU input and the BN-backward output gradient) and MNIST convT2 (GATHER)
+static const Ent k_pairs[] = {
+    CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 32, 2, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
+    CV_DUAL(OP_GATHER, CV_XF_BNBWD, CV_STAT_BWD, 64, 4, 64, 64, CV_XF_BNRELU, CV_XF_BNBWD, CV_STAT_NONE, 2, 0),
+};
+#undef CV_DUAL
+
+static const void* lookup(const int* dk, const int* gk) {
+  for (const Ent& e : k_pairs) {
+    bool ok = true;
+    for (int i = 0; i < 5; ++i) ok = ok && e.dk[i] == dk[i];
+    for (int i = 0; i < 7; ++i) ok = ok && e.gk[i] == gk[i];
+    if (ok) return e.fn;
+  }
+  return nullptr;
+}
+
+static int enabled() {  // CV_DUAL=0: back to back (A/B)
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CV_DUAL");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on;
+}
+
+static int launch_one(const void* kern, dim3 grid, size_t lds, void* arg, hipStream_t st, const char* what) {
+  void* params[] = {arg};
+  if (hipLaunchKernel(kern, grid, dim3(NT), params, lds, st) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("%s: launch failed", what);
+    return 2;
+  }
+  return 0;
+}
+
+}  // namespace dual
+
+// Issue the captured launches: one dual grid when the pair is served, else each on its own (direct first).
+static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
+  using namespace dual;
+  if (d.got && g.got && enabled()) {
+    const void* fn = lookup(d.key, g.key);
+    const long nd = (long)d.grid.x * d.grid.y, ng = (long)g.grid.x * g.grid.y * g.grid.z;
+    // (a direct grid of more than one resident round — VAE64's conv2 at 256 images, 1024 workgroups — measured
+    // slower as a dual grid, 174 -> 215 us; MNIST's pairs at 512 direct workgroups gain 4-5 us each)
+    if (fn && nd <= 512 && nd + ng < (1L << 31)) {
+      const size_t lds = d.lds > g.lds ? d.lds : g.lds;
+      bool ok = true;
+      if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = false;
+      }
+      if (ok) {
+        DualMap m{(int)nd, (int)d.grid.x, (int)d.grid.y, (int)ng, (int)g.grid.x, (int)g.grid.y, (int)g.grid.z};
+        void* params[] = {&d.a, &g.a, &m};
+        d.got = g.got = false;
+        if (hipLaunchKernel(fn, dim3((unsigned)(nd + ng)), dim3(NT), params, lds, st) != hipSuccess) {
+          (void)hipGetLastError();
+          set_error("dual launch failed");
+          return 2;
+        }
+        return 0;
+      }
+    }
+  }
+  int r = 0;
+  if (d.got) {
+    d.got = false;
+    r = launch_one(d.kern, d.grid, d.lds, &d.a, st, "direct conv");
+    if (r) return r;
+  }
+  if (g.got) {
+    g.got = false;
+    r = launch_one(g.kern, g.grid, g.lds, &g.a, st, "gemm");
+  }
+  return r;
+}
+
+static thread_local direct::DirectCap t_dcap;
+static thread_local fast::GemmCap t_gcap;
+
+void dual_begin() {
+  t_dcap = direct::DirectCap();
+  t_gcap = fast::GemmCap();
+  t_dcap.want = t_gcap.want = true;
+  direct::g_direct_cap = &t_dcap;
+  fast::g_gemm_cap = &t_gcap;
+}
+
+int dual_end(hipStream_t st, bool issue) {
+  direct::g_direct_cap = nullptr;
+  fast::g_gemm_cap = nullptr;
+  if (!issue) {  // (an error between begin and end: nothing captured is launched)
+    t_dcap.got = t_gcap.got = false;
+    return 0;
+  }
+  return dual_issue(t_dcap, t_gcap, st);
+}
+
+}  // namespace cv

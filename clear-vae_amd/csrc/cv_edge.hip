@@ -27,6 +27,25 @@ int wgrad_reduce_launch(const float* part, int split, int M, int N, int ntot, in
 
 namespace edge {
 
+#ifdef CV_STAMPS
+// instrumented builds only (make stamps): per-workgroup phase timeline [wg][8] u64 (s_memrealtime, 100 MHz),
+// the same layout as cv_direct.hip's: {entry, weights + constants, staged, MFMA done, stores issued, exit, HW_ID,
+// XCC_ID}
+static __device__ unsigned long long* g_estamps;
+#define CV_ESTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define CV_ESTAMP_WRITE()                                                                                 \
+  if (threadIdx.x == 0 && g_estamps) {                                                                    \
+    const unsigned long long st5 = __builtin_amdgcn_s_memrealtime();                                      \
+    unsigned long long* o = g_estamps + (size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 8;                \
+    o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st4; o[5] = st5;                               \
+    o[6] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));                                        \
+    o[7] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));                                       \
+  }
+#else
+#define CV_ESTAMP(v)
+#define CV_ESTAMP_WRITE()
+#endif
+
 constexpr int ET = 256;
 __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 constexpr int CS = 32;   // small-grid channels served
@@ -472,6 +491,7 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   const int n = blockIdx.y;
   const int nby = (g.hb - 1 + g.p) / 2 + 1, nbx = (g.wb - 1 + g.p) / 2 + 1;  // block rows / columns
   const int bb0 = blockIdx.x * P.rows;
+  CV_ESTAMP(st0);
   const int RBb = min(P.rows, nby - bb0);
   // small rows [ys_lo, ys_hi] feed block rows [bb0, bb0 + RBb); big rows [yb0, yb1) are the band's output
   const int ys_lo = max(bb0 - 1, 0), ys_hi = min(bb0 + RBb - 1, g.hs - 1);
@@ -508,6 +528,7 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   if (t < CB) sb[t] = P.bias ? P.bias[t] : 0.f;
   xf_consts(P.small, kf, kb, reinterpret_cast<double*>(sIn));  // (fold scratch: the staging area, unused yet)
   __syncthreads();
+  CV_ESTAMP(st1);
   float bw[4][8];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -523,6 +544,7 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
     stage_small<SP>(g, P.small, n, ys_lo * g.ws, nrs * g.ws, kf, kb, sIn);
   }
   __syncthreads();
+  CV_ESTAMP(st2);
   const float bias = nl < NCOL ? sb[cb] : 0.f;
   const int nblk = RBb * nbx, ntile = (nblk + 15) / 16;
   const FDiv fnbx = FDiv::make(nbx);
@@ -532,19 +554,25 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
     const int br = fnbx.div(blk), bx = blk - br * nbx, by = bb0 + br;
     // one accumulator per neighbour: four independent MFMA chains (a single chain of 32 dependent MFMAs
     // leaves the matrix pipe waiting on its own results), summed in neighbour order
-    f32x4 accq[4];
+    // (all four neighbours' fragments read first, then the chains interleaved neighbour-innermost: 32 MFMAs of
+    // which no two consecutive depend on each other — chained one neighbour at a time, every MFMA waited for
+    // the previous one's result)
+    f32x4 accq[4], a0[4], a1[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       accq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int ys = by - 1 + (q >> 1), xs = bx - 1 + (q & 1);
       const bool ok = blk < nblk && ys >= ys_lo && ys <= ys_hi && (unsigned)xs < (unsigned)g.ws;
       const float* ap = sIn + (ok ? ((ys - ys_lo) * g.ws + xs) * SP + 8 * kq : 0);  // (SP = 36: conflict-free)
-      f32x4 a0 = lds4(ap), a1 = lds4(ap + 4);
-      if (!ok) a0 = a1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int st = 0; st < 8; ++st)
-        accq[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(st < 4 ? a0[st] : a1[st - 4], bw[q][st], accq[q], 0, 0, 0);
+      a0[q] = lds4(ap);
+      a1[q] = lds4(ap + 4);
+      if (!ok) a0[q] = a1[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+#pragma unroll
+    for (int st = 0; st < 8; ++st)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        accq[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(st < 4 ? a0[q][st] : a1[q][st - 4], bw[q][st], accq[q], 0, 0, 0);
     const f32x4 acc = (accq[0] + accq[1]) + (accq[2] + accq[3]);
     // acc[r]: block 16 tile + 4 kq + r, column nl = (class, cb)
     if (nl < NCOL) {
@@ -560,6 +588,7 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
     }
   }
   __syncthreads();
+  CV_ESTAMP(st3);
   // the band's output rows are one contiguous range: 16-byte stores (+ the statistics epilogue)
   const int mode = P.ep.stat_mode;
   float s1[CB], s2[CB];
@@ -591,7 +620,11 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
         if (c == j) { s1[c] += v; s2[c] += v * v; }
     }
   }
+  CV_ESTAMP(st4);
   if (mode == CV_STAT_FWD) stats_out<CB>(s1, s2, P.ep.stat_out, CB, red);
+  if constexpr (!OUT) {
+    CV_ESTAMP_WRITE();
+  }
   if constexpr (OUT) {
     __shared__ BnFwdC ko[4];
     __shared__ double ored[ET / 64][1 + 2 * 4];
@@ -1071,6 +1104,12 @@ static bool geo_ok(const Geo& g) {
 }
 
 }  // namespace edge
+
+#ifdef CV_STAMPS
+extern "C" int cv_debug_set_stamps_edge(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(cv::edge::g_estamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 using namespace edge;
 

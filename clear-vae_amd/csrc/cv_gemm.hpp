@@ -238,17 +238,21 @@ __host__ __device__ inline size_t fast_lds_floats(int BM, int BN, int nfa, int n
 // MT: MMA_F32 (v_mfma_f32_16x16x4_f32, fp32 operands) or MMA_BF16 (operands rounded to bf16 when
 // staged into LDS after the fp32 transform, v_mfma_f32_16x16x32_bf16, fp32 accumulation)
 // (the deep-ring instances, D >= 4, serve under-filled launches only: 2 resident workgroups suffice there)
+// The one-tile body on the workgroup's block coordinates (bx0, by0, bz0) of a (gx0, gy0, gz0) grid: gemm_kernel's
+// own blockIdx, or its share of a dual launch (cv_dual.hip)
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
-__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? (D >= 4 ? 2 : CV_FAST_MINW_SMALL)
-                                                        : (BM == 64 ? CV_FAST_MINW_64 : 1))
-void gemm_kernel(const Args P) {
+__device__ __forceinline__ void gemm_body(const Args& P, const int bx0, const int by0, const int bz0, const int gx0,
+                                          const int gy0, const int gz0) {
+#define CV_GZ gz0
+#define CV_FIN_ME (unsigned)(bx0 + gx0 * (by0 + gy0 * bz0))
+#define CV_FIN_NBLK (unsigned)(gx0 * gy0 * gz0)
 #include "cv_gemm_prelude.inc"
 
   // ---------------- one tile per workgroup
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int nwg = gx * gy * gridDim.z;
-  const int hw_id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  const int gx = gx0, gy = gy0;
+  const int nwg = gx * gy * gz0;
+  const int hw_id = bx0 + gx * (by0 + gy * bz0);
+  int bx = bx0, by = by0, bz = bz0;
 #define CV_TILE_EXIT \
   do {              \
     finalize(true); \
@@ -262,6 +266,9 @@ void gemm_kernel(const Args P) {
 #undef CV_TILE_CONSTS_BEGIN
 #undef CV_TILE_CONSTS_END
 #undef CV_TILE_FINALIZE
+#undef CV_GZ
+#undef CV_FIN_ME
+#undef CV_FIN_NBLK
 #ifdef CV_STAMPS
   if (t == 0 && g_stamps) {
     const unsigned long long st3 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime();
@@ -271,6 +278,13 @@ void gemm_kernel(const Args P) {
     o[7] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
   }
 #endif
+}
+
+template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
+__global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? (D >= 4 ? 2 : CV_FAST_MINW_SMALL)
+                                                        : (BM == 64 ? CV_FAST_MINW_64 : 1))
+void gemm_kernel(const Args P) {
+  gemm_body<OP, BM, BN, XA, XB, EPI, D, MT>(P, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z);
 }
 
 // Two tiles per workgroup (GATHER / SCATTER launches with more tiles than one round of resident slots):
@@ -283,6 +297,9 @@ void gemm_kernel(const Args P) {
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int D, int MT>
 __global__ __launch_bounds__(NT, (BM == 64 && BN <= 32) ? 4 : (BM == 64 ? CV_FAST_MINW_64 : 1))
 void gemm_kernel2(const Args P) {
+#define CV_GZ ((int)gridDim.z)
+#define CV_FIN_ME (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z))
+#define CV_FIN_NBLK (gridDim.x * gridDim.y * gridDim.z)
 #include "cv_gemm_prelude.inc"
 
   const int gx = P.tiles_x, gy = P.tiles_y;
@@ -324,6 +341,9 @@ void gemm_kernel2(const Args P) {
   if (t1 >= 0) tile_body(t1);
   if (t2 >= 0) tile_body(t2);
   finalize(true);
+#undef CV_GZ
+#undef CV_FIN_ME
+#undef CV_FIN_NBLK
 }
 
 #ifndef CV_FAST_DEPTH_BNBWD
@@ -424,6 +444,18 @@ inline int xcd_wgrad_enabled() {
   return on;
 }
 
+// Launch capture (host): while `want` is set, the weight-gradient launch of launch_fast is recorded here instead
+// of issued (cv_dual.hip issues it beside a direct backward-data launch, or alone).
+struct GemmCap {
+  bool want = false, got = false;
+  int key[7];  // BM, BN, XA, XB, EPI, D, MT
+  Args a;
+  dim3 grid;
+  size_t lds = 0;
+  const void* kern = nullptr;
+};
+extern thread_local GemmCap* g_gemm_cap;
+
 template <int OP, int BM, int BN, int XA, int XB, int EPI, int MT>
 int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
   Args a = a0;
@@ -515,6 +547,17 @@ int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
         return 0;
       }
     }
+  }
+  if (OP == OP_WGRAD && g_gemm_cap && g_gemm_cap->want && !g_gemm_cap->got) {
+    GemmCap& c = *g_gemm_cap;
+    c.got = true;
+    const int key[7] = {BM, BN, XA, XB, EPI, DEPTH, MT};
+    for (int i = 0; i < 7; ++i) c.key[i] = key[i];
+    c.a = a;
+    c.grid = grid;
+    c.lds = lds;
+    c.kern = (const void*)kern;
+    return 0;
   }
   hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
   CV_LAUNCH_CHECK("gemm");

@@ -1533,11 +1533,15 @@ extern "C" int cv_conv_backward_deferred_kpack(const cv_conv* g, const cv_operan
                                                const float* wkpack, float* gin, const cv_epilogue* ep,
                                                const cv_operand* in, float* gweight, float* gbias, float* work,
                                                size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t stream) {
+  // the layer's backward-data and weight-gradient launches as one dual grid where the pair is served
+  // (cv_dual.hip); the image-side layer's fused edge launch and every other path launch as they are planned
+  dual_begin();
   g_wk = wkpack;
   const int r = cv_conv_backward_deferred(g, gout, wpacked, gin, ep, in, gweight, gbias, work, work_bytes, defer,
                                           stream);
   g_wk = nullptr;
-  return r;
+  const int r2 = dual_end(S(stream), r == 0);
+  return r ? r : r2;
 }
 
 // ---------------------------------------------------------------- linear layers

@@ -865,8 +865,14 @@ class Workspace:
             gout = operand(self.g_enc[li], XF_BNBWD, self.bn_enc[li].cv(True), y=self.y_enc[li])
             if li > 0:
                 ep = ep_bwd(self.bn_enc[li - 1], self.y_enc[li - 1], True)
-                P.add("cv_conv_backward_data_kpack", g, gout, c.wbwd, c.wfwd, self.g_enc[li - 1], ep)
                 xin = operand(self.y_enc[li - 1], XF_BNRELU, self.bn_enc[li - 1].cv(True))
+                if defer is not None and self.FUSED_EDGE_BWD:
+                    # backward-data + deferred weight gradient in one call: one dual launch where the pair is
+                    # served (cv_dual.hip)
+                    self._conv_backward(P, g, gout, c.wbwd, c.wfwd, self.g_enc[li - 1], ep, xin,
+                                        param_grad(c.mod.weight), ("enc", li), defer)
+                    continue
+                P.add("cv_conv_backward_data_kpack", g, gout, c.wbwd, c.wfwd, self.g_enc[li - 1], ep)
             else:
                 if dx is not None:
                     P.add("cv_conv_backward_data", g, gout, c.wbwd, dx, ep_none())

@@ -1,4 +1,5 @@
-"""Per-workgroup phase timeline of direct-conv calls INSIDE a step (stamps build, cv_direct.hip CV_STAMPS):
+"""Per-workgroup phase timeline of direct-conv (and edge_scatter: weights+constants, staged, MFMA, stores, stats)
+calls INSIDE a step (stamps build, cv_direct.hip CV_STAMPS):
 every call of the step before the target runs eagerly on the step stream, the stamp buffer is cleared, then the
 target call runs.  Phases: constants (entry -> BN constants staged), region (-> region staged and the ring's first
 stages landed), stages (-> last weight stage), epilogue (-> output stores issued), stats (-> exit).
@@ -17,10 +18,11 @@ res = bench.run_workload(cfgname, cfg, 0, 3, dev, 1, 0, detail=False)
 G = res["eng"].graphs[cfg[4]]
 L = _lib.lib()
 buf = torch.zeros(8 * 65536, dtype=torch.int64, device=dev)
-f = L.cv_debug_set_stamps_direct
-f.argtypes = [ctypes.c_void_p]
-f.restype = ctypes.c_int
-assert f(buf.data_ptr()) == 0
+for nm in ("cv_debug_set_stamps_direct", "cv_debug_set_stamps_edge"):
+    f = getattr(L, nm)
+    f.argtypes = [ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    assert f(buf.data_ptr()) == 0
 flat = []
 for pname, P in bench._programs(G):
     for i, c in enumerate(P.calls):
