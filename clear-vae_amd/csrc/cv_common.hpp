@@ -95,6 +95,8 @@ int direct_scatter(const Geo& g, const cv_operand* in, const float* wk, const fl
 // else back to back (issue = false: drops them, after an error)
 void dual_begin();
 int dual_end(hipStream_t st, bool issue);
+// the largest weight-gradient tile rows for the current capture (0: no cap)
+int dual_wgrad_bm_cap();
 int direct_gather(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,
                   const cv_epilogue* ep, hipStream_t st, int mma);
 

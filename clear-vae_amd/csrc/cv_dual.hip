@@ -27,6 +27,8 @@ thread_local DirectCap* g_direct_cap = nullptr;
 
 namespace dual {
 
+constexpr long kMaxDirect = 512;  // direct workgroups of a served dual grid (one resident round)
+
 struct DualMap {
   int nd, dgx, dgy;       // direct workgroups and their grid
   int ng, ggx, ggy, ggz;  // WGRAD workgroups and their grid
@@ -59,12 +61,14 @@ struct Ent {
 };
 #define CV_DUAL(a, b, c, d, e, f, g, h, i, j, k, l) \
   Ent{{a, b, c, d, e}, {f, g, h, i, j, k, l}, (const void*)dual_kernel<a, b, c, d, e, f, g, h, i, j, k, l>}
-// the pairs of the bench configurations' backward passes (fp32, 64-row WGRAD tiles: both roles fit two
-// workgroups per CU): MNIST / VAE64 conv2 (backward-data SCATTER with the BN-backward transform and STAT_BWD +
-// the weight gradient of the BN+ReLU input and the BN-backward output gradient) and MNIST convT2 (GATHER)
+// the pairs of the bench configurations' backward passes (fp32, 64-row WGRAD tiles — forced inside a dual capture,
+// dual_wgrad_bm_cap — so both roles fit two workgroups per CU): MNIST conv2 / conv3 (backward-data SCATTER with the
+// BN-backward transform and STAT_BWD + the weight gradient of the BN+ReLU input and the BN-backward output gradient)
+// and MNIST convT2 (GATHER)
 static const Ent k_pairs[] = {
     CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 32, 2, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
     CV_DUAL(OP_GATHER, CV_XF_BNBWD, CV_STAT_BWD, 64, 4, 64, 64, CV_XF_BNRELU, CV_XF_BNBWD, CV_STAT_NONE, 2, 0),
+    CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 64, 1, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
 };
 #undef CV_DUAL
 
@@ -107,7 +111,7 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
     const long nd = (long)d.grid.x * d.grid.y, ng = (long)g.grid.x * g.grid.y * g.grid.z;
     // (a direct grid of more than one resident round — VAE64's conv2 at 256 images, 1024 workgroups — measured
     // slower as a dual grid, 174 -> 215 us; MNIST's pairs at 512 direct workgroups gain 4-5 us each)
-    if (fn && nd <= 512 && nd + ng < (1L << 31)) {
+    if (fn && nd <= kMaxDirect && nd + ng < (1L << 31)) {
       const size_t lds = d.lds > g.lds ? d.lds : g.lds;
       bool ok = true;
       if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -142,6 +146,11 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
 
 static thread_local direct::DirectCap t_dcap;
 static thread_local fast::GemmCap t_gcap;
+
+int dual_wgrad_bm_cap() {
+  if (!direct::g_direct_cap || !t_dcap.got || !dual::enabled()) return 0;
+  return (long)t_dcap.grid.x * t_dcap.grid.y <= dual::kMaxDirect ? 64 : 0;
+}
 
 void dual_begin() {
   t_dcap = direct::DirectCap();

@@ -1203,6 +1203,10 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k) {
   WPlan w;
   const int Ntot = N + 1;
   w.BM = (M >= 128) ? 128 : 64;
+  // (inside a dual launch the weight gradient takes 64-row tiles: the 128-row tile's ~260 registers would hold the
+  // whole grid to one workgroup per CU)
+  const int cap = split_k <= 0 ? dual_wgrad_bm_cap() : 0;
+  if (cap && w.BM > cap) w.BM = cap;
   w.BN = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
   const long tiles = (long)cdiv(M, w.BM) * cdiv(Ntot, w.BN);
   const long ktiles = (K + BK - 1) / BK;
