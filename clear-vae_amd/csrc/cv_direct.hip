@@ -99,7 +99,12 @@ static bool plan(const Geo& g, int op, DArgs& a, int& cbt, long& nwg) {
   a.g = g;
   a.ci = sc ? g.cs : g.cb;
   a.co = sc ? g.cb : g.cs;
-  cbt = (a.co % 64 == 0) ? 64 : 32;
+  static int force32 = -1;  // CV_DIRECT_CBT32=1: 32-channel output tiles everywhere (A/B knob)
+  if (force32 < 0) {
+    const char* e = getenv("CV_DIRECT_CBT32");
+    force32 = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  cbt = (a.co % 64 == 0 && !force32) ? 64 : 32;
   a.nck = a.ci / CK;
   // taps per class, and the region offset of each: SCATTER output pixel Y = 2 by + dy reads small row
   // y = by + (dy + p - kh) / 2 for kh = dy + p (mod 2); GATHER output row y reads big row 2y - p + kh = plane
