@@ -274,7 +274,7 @@ def prefix_times(engine, G, labels, reps=20, rounds=3):
     return out
 
 
-def roofline_of(config, G, instep, precision, engine=None):
+def roofline_of(config, G, instep, precision, engine=None, world=1):
     """Roofline of the GEMM call with the largest in-step time.  Candidates are ranked by the eager
     in-step pass (whose event pairs add a few us per call); the top three are then re-timed inside a
     replayed graph of the step by prefix differences (prefix_times), and the largest wins."""
@@ -301,8 +301,11 @@ def roofline_of(config, G, instep, precision, engine=None):
             "frac": round(ach / peak, 4), "traffic": None, "kernel_ms": round(ms, 5), "flops_per_launch": fl,
             "timing": timing}
     # HBM bytes per launch of the same call from the committed rocprofv3 PMC passes
-    # (profiles/pmc_traffic.py), when they were taken on this call
+    # (profiles/pmc_traffic.py), when they were taken on this call (single-GPU programs: a data-parallel step's
+    # program labels index a different call list, so N > 1 keys carry no PMC figures)
     tpath = os.path.join(ROOT, "profiles", f"{config}_traffic.json")
+    if world > 1:
+        return roof
     if os.path.exists(tpath):
         try:
             t = json.load(open(tpath))["calls"].get(label)  # full "prog[i]:function" label of this build
@@ -472,7 +475,7 @@ def run_workload(name, cfg, steps, warmup, device, world, rank, detail=True, ker
         G = eng.graphs[B]
         instep = instep_pass(eng, G)
         res["instep"] = instep
-        res["roofline"] = roofline_of(name, G, instep, hp.get("precision", "fp32"), eng)
+        res["roofline"] = roofline_of(name, G, instep, hp.get("precision", "fp32"), eng, world)
         res["instep_sum_ms"] = sum(instep.values())
         if kernel_table and rank == 0:
             iso = isolated_pass(G)
