@@ -76,7 +76,7 @@ static const void* lookup(const int* dk, const int* gk) {
   for (const Ent& e : k_pairs) {
     bool ok = true;
     for (int i = 0; i < 5; ++i) ok = ok && e.dk[i] == dk[i];
-    for (int i = 0; i < 7; ++i) ok = ok && e.gk[i] == gk[i];
+    for (int i = 0; i < 7 && gk; ++i) ok = ok && e.gk[i] == gk[i];  // (gk null: any weight-gradient side)
     if (ok) return e.fn;
   }
   return nullptr;
@@ -147,9 +147,9 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
 static thread_local direct::DirectCap t_dcap;
 static thread_local fast::GemmCap t_gcap;
 
-int dual_wgrad_bm_cap() {
+int dual_wgrad_bm_cap() {  // (only when the captured direct launch belongs to a served pair)
   if (!direct::g_direct_cap || !t_dcap.got || !dual::enabled()) return 0;
-  return (long)t_dcap.grid.x * t_dcap.grid.y <= dual::kMaxDirect ? 64 : 0;
+  return ((long)t_dcap.grid.x * t_dcap.grid.y <= dual::kMaxDirect && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
 }
 
 void dual_begin() {
