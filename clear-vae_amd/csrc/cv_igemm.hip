@@ -1198,36 +1198,49 @@ struct WPlan {
 
 // Split-K plan of a WGRAD problem (independent of whether a bias column is present, so the
 // workspace query and the launch agree): ~1024 workgroups, >= 8 K tiles per split (>= 4 when the
-// problem would otherwise not fill the 256 CUs).
+// problem would otherwise not fill the 256 CUs).  128-row tiles when M allows, unless their grid would hold
+// <= 2 workgroups per CU (few K tiles: MNIST's conv3-sized gradients, VAE64's conv5): then 64-row tiles, twice
+// the workgroups (MNIST decoder convT1 gradient 37.2 -> 35.0 us, VAE64 conv5 pair 200.6 -> 195.3 us; applied
+// everywhere they cost VAE64's 1024-workgroup gradients ~7 us each).
 static WPlan wgrad_plan(int M, int N, long K, int split_k) {
   WPlan w;
   const int Ntot = N + 1;
-  w.BM = (M >= 128) ? 128 : 64;
-  // (inside a dual launch the weight gradient takes 64-row tiles: the 128-row tile's ~260 registers would hold the
-  // whole grid to one workgroup per CU)
-  const int cap = split_k <= 0 ? dual_wgrad_bm_cap() : 0;
-  if (cap && w.BM > cap) w.BM = cap;
   w.BN = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
-  const long tiles = (long)cdiv(M, w.BM) * cdiv(Ntot, w.BN);
   const long ktiles = (K + BK - 1) / BK;
-  long split;
-  if (split_k > 0) {
-    split = split_k;
-  } else {
-    static long target = -1;  // A/B override: CV_WGRAD_TARGET (workgroups the split aims for)
-    if (target < 0) {
-      const char* e = getenv("CV_WGRAD_TARGET");
-      target = e ? atol(e) : 1024;
-      if (target < 1) target = 1024;
-    }
-    split = (target + tiles - 1) / tiles;
+  static long target = -1;  // A/B override: CV_WGRAD_TARGET (workgroups the split aims for)
+  static int bm_ovr = -2;   // A/B override: CV_WGRAD_BM = 64 / 128 (row tile whenever M allows)
+  if (target < 0) {
+    const char* e = getenv("CV_WGRAD_TARGET");
+    target = e ? atol(e) : 1024;
+    if (target < 1) target = 1024;
+    e = getenv("CV_WGRAD_BM");
+    bm_ovr = e ? atoi(e) : -1;
+  }
+  auto split_for = [&](int bm) -> long {
+    if (split_k > 0) return split_k > 4096 ? 4096 : split_k;
+    const long tiles = (long)cdiv(M, bm) * cdiv(Ntot, w.BN);
+    long split = (target + tiles - 1) / tiles;
     long maxs = ktiles / 8;
     if (tiles * maxs < 256) maxs = ktiles / 4;
     if (maxs < 1) maxs = 1;
     if (split > maxs) split = maxs;
     if (split < 1) split = 1;
+    return split > 4096 ? 4096 : split;
+  };
+  w.BM = (M >= 128) ? 128 : 64;
+  // (inside a dual launch the weight gradient takes 64-row tiles: the 128-row tile's ~260 registers would hold the
+  // whole grid to one workgroup per CU)
+  const int cap = split_k <= 0 ? dual_wgrad_bm_cap() : 0;
+  if (cap && w.BM > cap) w.BM = cap;
+  if (w.BM == 128) {
+    if (bm_ovr == 64) {
+      w.BM = 64;
+    } else if (bm_ovr != 128 && split_k <= 0) {
+      const long wgs = (long)cdiv(M, 128) * cdiv(Ntot, w.BN) * split_for(128);
+      if (wgs <= 512) w.BM = 64;  // (2 x the 256 CUs; a constant, so the workspace query needs no device)
+    }
   }
-  if (split > 4096) split = 4096;
+  const long split = split_for(w.BM);
   w.kchunk = (int)(((K + split - 1) / split + BK - 1) / BK) * BK;
   w.split = (int)((K + w.kchunk - 1) / w.kchunk);
   return w;
