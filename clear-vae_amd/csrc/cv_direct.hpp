@@ -249,7 +249,11 @@ __device__ __forceinline__ void direct_body(const DArgs& P, const int bx, const 
 #pragma unroll
       for (int i = 0; i < FMX; ++i) eyv[c][i] = fast::g4(P.ep.ey + (pix_ok(c, i) ? ob[i] + cofs(c) : 0));
   }
-  __syncthreads();  // region visible (and the ring's first NSL - 1 stages landed)
+  // The ring's first NSL - 1 stages landed: an explicit count, so the first fragment read below does not depend on
+  // how the barrier's fence is lowered for LDS-DMA.  Only the NC * FMX pre-BN loads issued after the DMA may
+  // remain in flight (vector-memory loads retire in order).
+  wait_vm(EPI == CV_STAT_BWD ? NC * FMX : 0);
+  __syncthreads();  // region visible
   CV_DSTAMP(st2);
 
   f32x4 acc[NC][FMX];

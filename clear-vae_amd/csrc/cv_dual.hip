@@ -82,13 +82,15 @@ static const void* lookup(const int* dk, const int* gk) {
   return nullptr;
 }
 
-static int enabled() {  // CV_DUAL=0: back to back (A/B)
-  static int on = -1;
-  if (on < 0) {
+static int g_on = -1;     // CV_DUAL=0: back to back (A/B); cv_debug_dual overrides
+static int g_issued = 0;  // dual grids issued (test hook cv_debug_dual_count)
+
+static int enabled() {
+  if (g_on < 0) {
     const char* e = getenv("CV_DUAL");
-    on = (e && atoi(e) == 0) ? 0 : 1;
+    g_on = (e && atoi(e) == 0) ? 0 : 1;
   }
-  return on;
+  return g_on;
 }
 
 static int launch_one(const void* kern, dim3 grid, size_t lds, void* arg, hipStream_t st, const char* what) {
@@ -127,6 +129,7 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
           set_error("dual launch failed");
           return 2;
         }
+        ++g_issued;
         return 0;
       }
     }
@@ -171,3 +174,15 @@ int dual_end(hipStream_t st, bool issue) {
 }
 
 }  // namespace cv
+
+extern "C" int cv_debug_dual(int on) {
+  const int prev = cv::dual::enabled();
+  if (on >= 0) cv::dual::g_on = on ? 1 : 0;
+  return prev;
+}
+
+extern "C" int cv_debug_dual_count(int reset) {
+  const int n = cv::dual::g_issued;
+  if (reset) cv::dual::g_issued = 0;
+  return n;
+}

@@ -1202,7 +1202,8 @@ struct WPlan {
 // <= 2 workgroups per CU (few K tiles: MNIST's conv3-sized gradients, VAE64's conv5): then 64-row tiles, twice
 // the workgroups (MNIST decoder convT1 gradient 37.2 -> 35.0 us, VAE64 conv5 pair 200.6 -> 195.3 us; applied
 // everywhere they cost VAE64's 1024-workgroup gradients ~7 us each).
-static WPlan wgrad_plan(int M, int N, long K, int split_k) {
+// cap_ovr >= 0 replaces the dual-capture row cap (the workspace query takes the max over both choices).
+static WPlan wgrad_plan(int M, int N, long K, int split_k, int cap_ovr = -1) {
   WPlan w;
   const int Ntot = N + 1;
   w.BN = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
@@ -1230,7 +1231,7 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k) {
   w.BM = (M >= 128) ? 128 : 64;
   // (inside a dual launch the weight gradient takes 64-row tiles: the 128-row tile's ~260 registers would hold the
   // whole grid to one workgroup per CU)
-  const int cap = split_k <= 0 ? dual_wgrad_bm_cap() : 0;
+  const int cap = split_k > 0 ? 0 : cap_ovr >= 0 ? cap_ovr : dual_wgrad_bm_cap();
   if (cap && w.BM > cap) w.BM = cap;
   if (w.BM == 128) {
     if (bm_ovr == 64) {
@@ -1246,9 +1247,16 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k) {
   return w;
 }
 
+// Queried outside any capture, so it must cover both row tiles a launch may take: the plain plan and the one capped
+// at 64 rows inside a dual grid (today the capped split never exceeds the uncapped one, but nothing forces that).
 static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
-  const WPlan w = wgrad_plan(M, N, K, split_k);
-  return w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
+  size_t b = 0;
+  for (int cap : {0, 64}) {
+    const WPlan w = wgrad_plan(M, N, K, split_k, cap);
+    const size_t need = w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
+    if (need > b) b = need;
+  }
+  return b;
 }
 
 // Deferred weight gradients (cv_*_backward_weight_deferred): while a sink is set, the split-K partial

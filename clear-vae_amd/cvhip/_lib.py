@@ -340,6 +340,8 @@ _SIGS = {
     "cv_debug_direct_count": (c_int, [c_int]),
     "cv_debug_direct_minwg": (c_int, [c_int]),
     "cv_debug_direct_gather_rule": (c_int, [c_int]),
+    "cv_debug_dual": (c_int, [c_int]),
+    "cv_debug_dual_count": (c_int, [c_int]),
     "cv_gemm_workspace_bytes": (c_size_t, []),
     "cv_set_gemm_workspace": (c_int, [c_void_p, c_size_t]),
 }

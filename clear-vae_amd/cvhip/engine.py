@@ -642,6 +642,10 @@ class ClearStep:
         all-reduced under DP — and before the Adam launch; such a step runs eagerly, not from the graph (used by
         the tests to read the step's activations with the pre-update parameters)."""
         n = X.shape[0]
+        if before_update is not None and FUSED_ADAM and self.world == 1:
+            # (Adam rides in the reduction launch of the `enc` program: there is no point between the complete
+            # gradients and the update at which the hook could run)
+            raise RuntimeError("before_update is not supported with CVHIP_FUSED_ADAM=1")
         G = self.graphs.get(n)
         if G is None:
             G = self._programs(n)

@@ -542,6 +542,12 @@ int cv_debug_direct_minwg(int minwg);
  * core (one resident round of workgroups, >= 32 output pixels per tile); 0 serves every geometry it can plan
  * (kernel tests); returns the previous setting */
 int cv_debug_direct_gather_rule(int on);
+/* test hook: 1 (default) issues a served backward-data + weight-gradient pair as one dual grid (cv_dual.hip), 0 runs
+ * the two launches back to back (the arithmetic of each role is the same); a negative value only queries; returns
+ * the previous setting */
+int cv_debug_dual(int on);
+/* test hook: dual grids issued since the last reset */
+int cv_debug_dual_count(int reset);
 
 /* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
  * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least

@@ -157,8 +157,12 @@ def test_bf16_step_mask_pinned(arch, zt, C, n):
 # points) lands 1e-3 - 6e-3 from its fp64 evaluation per gradient tensor (measured; the fp32 "floor").  The device
 # can be no closer; the bars hold it to that floor: every tensor within max(1e-3, PIN_FLOOR_X x its floor) and the
 # median tensor within max(1e-4, PIN_FLOOR_X x the median floor).  (A wrong bf16 weight gradient on any tensor
-# is off by O(1), far outside.)
-PIN_FLOOR_X = 2.0
+# is off by O(1), far outside.)  On top, a fixed cap PIN_CAP on every tensor, whatever its floor.  The cap is 1e-2,
+# not 5e-3: the floor itself reaches 8.0e-3 (VAE64 n=32 encoder.1.weight; the per-tensor table is in DESIGN.md §2),
+# so no fp32 evaluation of this function passes 5e-3 on every tensor.  Measured device / floor ratios are
+# 0.5-1.3 (round 5), so PIN_FLOOR_X is 1.5 (was 2).
+PIN_FLOOR_X = 1.5
+PIN_CAP = 1e-2
 
 
 def _check_bf16_pinned(got, ref64, ref32, arch, what):
@@ -169,13 +173,15 @@ def _check_bf16_pinned(got, ref64, ref32, arch, what):
         r = _rel(got[k], g_ref.detach())
         floor = _rel(ref32[k].detach().double(), g_ref.detach())
         rels.append((r, k, floor))
-        if r >= max(1e-3, PIN_FLOOR_X * floor):
+        if r >= min(PIN_CAP, max(1e-3, PIN_FLOOR_X * floor)):
             over.append((k, r, floor))
     rels.sort()
     med = rels[len(rels) // 2][0]
     fmed = sorted(f for _, _, f in rels)[len(rels) // 2]
     print(f"\n{what} bf16 pinned: median {med:.2e} (floor median {fmed:.2e}); worst (rel, tensor, fp32 floor): "
           + ", ".join(f"({r:.1e}, {k}, {f:.1e})" for r, k, f in rels[-3:]))
+    print(f"{what} per-tensor table (rel, fp32 floor): "
+          + "; ".join(f"{k} {r:.2e} {f:.2e}" for r, k, f in sorted(rels, key=lambda v: v[1])))
     assert med < max(1e-4, PIN_FLOOR_X * fmed), (med, fmed, rels[-3:])
     assert not over, over
 
