@@ -300,17 +300,26 @@ def roofline_of(config, G, instep, precision, engine=None, world=1):
     roof = {"bound": "mfma", "kernel": label, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": None, "kernel_ms": round(ms, 5), "flops_per_launch": fl,
             "timing": timing}
+    # the kernels this call really issues (cv_debug_kernel_log around one more eager launch of it): a PMC figure
+    # below is attached only if it was taken on exactly these kernels
+    ran = call_kernels(G, label) if engine is not None and world == 1 else None
+    if ran is not None:
+        roof["kernels"] = ran
     # HBM bytes per launch of the same call from the committed rocprofv3 PMC passes
     # (profiles/pmc_traffic.py), when they were taken on this call (single-GPU programs: a data-parallel step's
     # program labels index a different call list, so N > 1 keys carry no PMC figures)
     tpath = os.path.join(ROOT, "profiles", f"{config}_traffic.json")
     if world > 1:
         return roof
+    stale = {}
     if os.path.exists(tpath):
         try:
             t = json.load(open(tpath))["calls"].get(label)  # full "prog[i]:function" label of this build
             if t is not None:
-                roof["traffic"] = round(float(t["traffic_bytes"]))
+                if ran is not None and _knorm(t.get("kernels", [])) != _knorm(ran):
+                    stale["traffic_kernels"] = t.get("kernels", [])
+                else:
+                    roof["traffic"] = round(float(t["traffic_bytes"]))
         except (OSError, ValueError, KeyError):
             pass
     # MFMA utilisation of the same call from the committed counter pass (profiles/pmc_mfma.py), when taken
@@ -318,13 +327,61 @@ def roofline_of(config, G, instep, precision, engine=None, world=1):
     if os.path.exists(upath):
         try:
             key = f"{config} {label.split(':', 1)[0]}"
-            for line in open(upath):
+            for line in open(upath):  # (the last entry of a key wins)
                 u = json.loads(line).get(key)
-                if u is not None:
+                if u is None:
+                    continue
+                if ran is not None and _knorm(u.get("kernels", [])) != _knorm(ran):
+                    stale["mfma_util_kernels"] = u.get("kernels", [])
+                    roof.pop("mfma_util_pmc", None)
+                else:
+                    stale.pop("mfma_util_kernels", None)
                     roof["mfma_util_pmc"] = round(float(u["mfma_util_median"]), 4)
         except (OSError, ValueError, KeyError):
             pass
+    if stale:  # (refused: the committed counters describe other kernels than the ones timed)
+        roof["pmc_refused"] = stale
     return roof
+
+
+def _knorm(names):
+    """Kernel names without return type, parameter list and spaces (rocprofv3 and __cxa_demangle spell them alike,
+    up to whitespace)."""
+    out = []
+    for n in names:
+        n = n.strip()
+        if n.startswith("void "):
+            n = n[5:]
+        if n.endswith(")") and "(" in n:
+            n = n[:n.rindex("(")]
+        out.append(n.replace(" ", ""))
+    return out
+
+
+def call_kernels(G, label):
+    """Demangled names of the kernels one eager launch of the step-program call `label` issues (mutates the
+    workspace: run after timing)."""
+    import ctypes
+
+    from cvhip import _lib
+
+    pname, rest = label.split("[", 1)
+    P = dict(_programs(G)).get(pname)
+    if P is None:
+        return None
+    name, fn, cargs, _lane = P.calls[int(rest.split("]")[0])]
+    L = _lib.lib()
+    torch.cuda.synchronize()
+    prev = L.cv_debug_kernel_log(1)
+    try:
+        _lib.check(fn(*cargs, _lib.stream_handle()), name)
+        torch.cuda.synchronize()
+        buf = ctypes.create_string_buffer(1 << 16)
+        n = L.cv_debug_kernel_names(buf, len(buf))
+    finally:
+        L.cv_debug_kernel_log(prev)
+    names = buf.value.decode().split("\n") if n else []
+    return names
 
 
 def cpu_model():

@@ -13,6 +13,8 @@ namespace cv {
 
 // ---------------------------------------------------------------- host error plumbing
 void set_error(const char* fmt, ...);
+// launch log (cv_debug_kernel_log): the conv / linear launch sites record the kernel they issue
+void note_launch(const void* kernel);
 void clear_error();
 
 #define CV_REQUIRE(cond, ...)                \

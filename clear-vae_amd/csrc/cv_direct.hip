@@ -312,6 +312,7 @@ static int direct_run(int op, const Geo& g, const cv_operand* in, const float* w
     return 0;
   }
   void* params[] = {&a};
+  note_launch(kern);
   if (hipLaunchKernel(kern, grid, dim3(NT), params, lds, st) != hipSuccess) {
     (void)hipGetLastError();
     set_error("direct conv: launch failed");

@@ -95,6 +95,7 @@ static int enabled() {
 
 static int launch_one(const void* kern, dim3 grid, size_t lds, void* arg, hipStream_t st, const char* what) {
   void* params[] = {arg};
+  note_launch(kern);
   if (hipLaunchKernel(kern, grid, dim3(NT), params, lds, st) != hipSuccess) {
     (void)hipGetLastError();
     set_error("%s: launch failed", what);
@@ -124,6 +125,7 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
         DualMap m{(int)nd, (int)d.grid.x, (int)d.grid.y, (int)ng, (int)g.grid.x, (int)g.grid.y, (int)g.grid.z};
         void* params[] = {&d.a, &g.a, &m};
         d.got = g.got = false;
+        note_launch(fn);
         if (hipLaunchKernel(fn, dim3((unsigned)(nd + ng)), dim3(NT), params, lds, st) != hipSuccess) {
           (void)hipGetLastError();
           set_error("dual launch failed");

@@ -1078,6 +1078,7 @@ static int launch(const void* kern, dim3 grid, size_t lds, const EArgs& a, hipSt
   }
   EArgs arg = a;
   void* params[] = {&arg};
+  note_launch(kern);
   if (hipLaunchKernel(kern, grid, dim3(ET), params, lds, st) != hipSuccess) {
     (void)hipGetLastError();
     set_error("%s: launch failed", what);
@@ -1241,6 +1242,7 @@ static int edge_scatter_impl(const Geo& g, const cv_operand* in, const float* ws
   }
   EArgs arg = a;
   void* params[] = {&arg, &oa};
+  note_launch(kern);
   if (hipLaunchKernel(kern, grid, dim3(ET), params, lds, st) != hipSuccess) {
     (void)hipGetLastError();
     set_error("edge_scatter: launch failed");
@@ -1343,6 +1345,7 @@ int edge_bwd(const Geo& g, const cv_operand* gout, const float* wg, float* gin, 
     return 1;
   }
   void* params[] = {&a, &b};
+  note_launch(kern);
   if (hipLaunchKernel(kern, dim3(cdiv(g.hs, a.rows), g.n), dim3(ET), params, lds, st) != hipSuccess) {
     (void)hipGetLastError();
     set_error("edge_bwd: launch failed");

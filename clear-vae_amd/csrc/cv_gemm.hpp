@@ -501,6 +501,7 @@ int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
     if (slots1 > 0 && tiles * deep_den() <= slots1 * deep_num()) {
       auto kern4 = gemm_kernel<OP, BM, BN, XA, XB, EPI, CV_FAST_DEPTH_DEEP, MT>;
       if (carve((const void*)kern4)) return 1;
+      note_launch((const void*)kern4);
       hipLaunchKernelGGL(kern4, grid, dim3(NT), lds, st, a);
       CV_LAUNCH_CHECK("gemm_deep");
       return 0;
@@ -542,6 +543,7 @@ int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
             for (int i = 0; i < ncls; ++i) p.cls_order[i] = ord[i];
           }
         }
+        note_launch((const void*)kern2);
         hipLaunchKernelGGL(kern2, dim3((unsigned)G), dim3(NT), lds, st, p);
         CV_LAUNCH_CHECK("gemm2");
         return 0;
@@ -559,6 +561,7 @@ int launch_fast(const Args& a0, dim3 grid, hipStream_t st) {
     c.kern = (const void*)kern;
     return 0;
   }
+  note_launch((const void*)kern);
   hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
   CV_LAUNCH_CHECK("gemm");
   return 0;

@@ -812,6 +812,7 @@ static int launch_t(const Args& a, dim3 grid, hipStream_t st) {
       return 1;
     }
   }
+  note_launch((const void*)igemm_kernel<OP, BM, BN>);
   hipLaunchKernelGGL((igemm_kernel<OP, BM, BN>), grid, dim3(NT), lds, st, a);
   CV_LAUNCH_CHECK("igemm");
   return 0;
@@ -1283,6 +1284,7 @@ static int launch_wgrad_reduce(const float* part, int split, int M, int N, int n
   int gy = cdiv(split, 32);  // <= 32 slabs per block (8 per thread)
   const int zper = cdiv(split, gy);
   gy = cdiv(split, zper);
+  note_launch((const void*)wgrad_reduce_kernel);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, part, split, zper, M, N, ntot, cb, kk, gw,
                      gbias);
   CV_LAUNCH_CHECK("wgrad_reduce");

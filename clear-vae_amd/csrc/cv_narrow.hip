@@ -380,6 +380,7 @@ int narrow_gather(const Geo& g, const cv_operand* in, const float* wg, const flo
   long blocks = (a.M + 31) / 32;  // 32 pixels per block iteration
   if (blocks > 1024) blocks = 1024;
   const dim3 grid((int)blocks), blk(NNT);
+  note_launch(g.kh == 3 ? (const void*)narrow_gather_kernel<32, 3, 1> : (const void*)narrow_gather_kernel<32, 4, 1>);
   if (g.kh == 3) hipLaunchKernelGGL((narrow_gather_kernel<32, 3, 1>), grid, blk, 0, st, a);
   else hipLaunchKernelGGL((narrow_gather_kernel<32, 4, 1>), grid, blk, 0, st, a);
   CV_LAUNCH_CHECK("narrow_gather");
@@ -406,7 +407,7 @@ int narrow_scatter(const Geo& g, const cv_operand* in, const float* ws, const fl
   long bx = (rows + 63) / 64;  // 64 pixels per block iteration
   if (bx > 512) bx = 512;       // bounds the fp64 atomics per statistics address
   const dim3 grid((int)bx, g.s * g.s), blk(NNT);
-#define CV_NS(CBV) hipLaunchKernelGGL((narrow_scatter_kernel<CBV, 2>), grid, blk, 0, st, a)
+#define CV_NS(CBV) do { note_launch((const void*)narrow_scatter_kernel<CBV, 2>); hipLaunchKernelGGL((narrow_scatter_kernel<CBV, 2>), grid, blk, 0, st, a); } while (0)
   switch (g.cb) {
     case 1: CV_NS(1); break;
     case 2: CV_NS(2); break;

@@ -2,7 +2,11 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <cxxabi.h>
+#include <stdlib.h>
 #include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
 #include "../../include/clearvae.h"
 
 namespace cv {
@@ -19,6 +23,43 @@ void clear_error() { g_err[0] = 0; }
 
 extern "C" const char* cv_last_error(void) { return cv::g_err; }
 extern "C" int cv_version(void) { return 1; }
+
+// ---- launch log: which kernels a call really issued (bench.py checks that the PMC passes it quotes were taken on
+// the kernels the timed call runs)
+namespace cv {
+static thread_local bool t_klog = false;
+static thread_local std::vector<const void*> t_klaunch;
+void note_launch(const void* kernel) {
+  if (t_klog) t_klaunch.push_back(kernel);
+}
+}  // namespace cv
+
+extern "C" int cv_debug_kernel_log(int on) {
+  const int prev = cv::t_klog ? 1 : 0;
+  cv::t_klog = on != 0;
+  cv::t_klaunch.clear();
+  return prev;
+}
+
+extern "C" int cv_debug_kernel_names(char* buf, size_t cap) {
+  std::string all;
+  for (const void* k : cv::t_klaunch) {
+    const char* m = hipKernelNameRefByPtr(k, nullptr);
+    std::string name = m ? m : "?";
+    int st = 0;
+    char* d = (m && m[0] == '_' && m[1] == 'Z') ? abi::__cxa_demangle(m, nullptr, nullptr, &st) : nullptr;
+    if (d && st == 0) name = d;
+    free(d);
+    if (!all.empty()) all += '\n';
+    all += name;
+  }
+  if (buf && cap) {
+    const size_t n = all.size() < cap - 1 ? all.size() : cap - 1;
+    memcpy(buf, all.data(), n);
+    buf[n] = 0;
+  }
+  return (int)cv::t_klaunch.size();
+}
 
 extern "C" int cv_zero(void* ptr, size_t bytes, cv_stream_t stream) {
   cv::clear_error();

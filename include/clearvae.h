@@ -548,6 +548,12 @@ int cv_debug_direct_gather_rule(int on);
 int cv_debug_dual(int on);
 /* test hook: dual grids issued since the last reset */
 int cv_debug_dual_count(int reset);
+/* measurement hook: 1 starts recording (on this thread) the kernels the conv / linear calls launch, clearing the
+ * record; 0 stops; returns the previous setting.  cv_debug_kernel_names writes the recorded kernels' demangled
+ * names, one per line, into buf (truncated to cap - 1 bytes, NUL-terminated) and returns how many were recorded
+ * (bench.py: the PMC passes a roofline quotes must have been taken on the kernels the priced call issues). */
+int cv_debug_kernel_log(int on);
+int cv_debug_kernel_names(char* buf, size_t cap);
 
 /* ---- GEMM workspace (in-launch split-K of under-filled long-K conv forward / ConvT backward-data
  * launches, e.g. VAE64's conv5 at 32-256 images per GPU): a caller-owned device buffer of at least
