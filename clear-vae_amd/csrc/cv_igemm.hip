@@ -840,6 +840,7 @@ static void finalize_divs(Args& a) {
   a.f_opix = FDiv::make(a.o_pix);
   a.f_sdiv = FDiv::make(a.ep.stat_div);
   a.f_s = FDiv::make(a.g.s);
+  a.f_n = FDiv::make(a.g.n);
 }
 
 // 1: route every call to the generic kernel (kernel-variant comparisons in tests only)
@@ -1054,6 +1055,30 @@ static int gather_split(long tiles, int ktiles) {
   return s;
 }
 
+// Pixel-major tiles (Args::pm, cv_gemm_tile.inc) when they pay: the conv's (small pixel, tap) pairs that land in
+// the padding — zero products the image-major tiles issue anyway — are >= 10 % of all pairs (VAE64's conv5 / convT1:
+// 2x2 <-> 4x4, 28 of 64; conv4 / convT2: 60 of 256; MNIST's conv3 / convT1: 44 of 144), the tile divides the batch
+// (rows_tile: BM rows of GATHER / SCATTER, BK K elements of WGRAD) and <= 16 taps / small pixels fit the tile's
+// 4-bit lists.  CV_PM=0: off (A/B).
+static int g_pm_mode = -1;     // (cv_debug_pm)
+static int g_pm_launches = 0;  // calls that took pixel-major tiles (cv_debug_pm_count)
+static bool pm_pays(const Geo& g, int rows_tile) {
+  if (g_pm_mode < 0) {
+    const char* e = getenv("CV_PM");
+    g_pm_mode = e ? atoi(e) : 1;
+  }
+  if (!g_pm_mode || g_force_generic || rows_tile <= 0 || g.n % rows_tile || g.kh * g.kw > 16) return false;
+  long valid = 0;
+  for (int ys = 0; ys < g.hs; ++ys)
+    for (int xs = 0; xs < g.ws; ++xs)
+      for (int kh = 0; kh < g.kh; ++kh)
+        for (int kw = 0; kw < g.kw; ++kw)
+          valid += ((unsigned)(ys * g.s - g.p + kh) < (unsigned)g.hb && (unsigned)(xs * g.s - g.p + kw) < (unsigned)g.wb);
+  const bool on = 10 * valid <= 9L * g.hs * g.ws * g.kh * g.kw;
+  g_pm_launches += on ? 1 : 0;
+  return on;
+}
+
 // the other packing of the current call's weights (cv_conv_*_kpack: the k-contiguous B image of the direct
 // kernels, [tap][co][ci]), else null
 static thread_local const float* g_wk = nullptr;
@@ -1115,6 +1140,7 @@ static int run_gather(const Geo& g, const cv_operand* in, const float* w, const 
       BN_ = 64;
     }
   }
+  a.pm = (g.cb % BK == 0 && pm_pays(g, BM_)) ? 1 : 0;
   const long tiles = (long)cdiv(a.M, BM_) * cdiv(a.N, BN_);
   const int split = (a.K % BK == 0) ? gather_split(tiles, a.K / BK) : 1;
   float* part = nullptr;
@@ -1162,6 +1188,7 @@ static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const
   if (apply_epilogue(a, ep, a.N, what)) return 1;
   int BM_, BN_;
   pick_tile((long)a.M * g.s * g.s, a.N, BM_, BN_);
+  a.pm = (g.cs % BK == 0 && pm_pays(g, BM_)) ? 1 : 0;
   // in-launch split-K as in run_gather, for kernels whose stride-parity classes all have the same taps
   // (kh, kw multiples of the stride: every class has K = a.K) and even class extents
   const int ss = g.s * g.s;
@@ -1337,6 +1364,9 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
     }
   }
   a.kchunk = w.kchunk;
+  // pixel-major K (a K tile = 32 images at one small pixel; an N tile = one tap): the tile skips the pixels at which
+  // its tap reads padding (the split is then re-cut per tile over the pixels it visits)
+  a.pm = (!gbias && g.cb % w.BN == 0 && g.hs * g.ws <= 16 && pm_pays(g, BK)) ? 1 : 0;
   static int atomic_splits = -1;  // A/B knob CV_WGRAD_ATOMIC=1: split-K tiles added with fp32 atomics, no partials
   if (atomic_splits < 0) {
     const char* e = getenv("CV_WGRAD_ATOMIC");
@@ -1371,6 +1401,18 @@ extern "C" int cv_set_gemm_workspace(void* work, size_t bytes) {
   g_fix_work[dev] = work;
   g_fix_bytes[dev] = work ? bytes : 0;
   return 0;
+}
+
+extern "C" int cv_debug_pm(int on) {
+  const int prev = g_pm_mode;
+  if (on >= 0) g_pm_mode = on ? 1 : 0;
+  return prev;
+}
+
+extern "C" int cv_debug_pm_count(int reset) {
+  const int n = g_pm_launches;
+  if (reset) g_pm_launches = 0;
+  return n;
 }
 
 extern "C" int cv_debug_force_generic_gemm(int on) {

@@ -64,8 +64,12 @@ struct Args {
   // taps, heaviest first; 0 classes: identity order
   int bal_ncls;
   int cls_order[4];
+  // pixel-major tiles (specialised core, cv_gemm_tile.inc): GATHER / SCATTER rows, WGRAD K index ordered
+  // pixel-major (r = pixel * n + image) instead of image-major, so a tile of BM | n rows (a K tile of BK | n) sits
+  // at ONE pixel; the conv's padding taps (or pixels) are then the same for the whole tile and its K loop skips them
+  int pm;
   // fast divisors (filled by finalize_divs at launch)
-  FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s;
+  FDiv f_cb, f_cs, f_kw, f_ws, f_hws, f_ach, f_opix, f_sdiv, f_s, f_n;
 };
 
 // ------------------------------------------------------------------ operand transform helpers

@@ -341,6 +341,8 @@ _SIGS = {
     "cv_debug_direct_minwg": (c_int, [c_int]),
     "cv_debug_direct_gather_rule": (c_int, [c_int]),
     "cv_debug_dual": (c_int, [c_int]),
+    "cv_debug_pm": (c_int, [c_int]),
+    "cv_debug_pm_count": (c_int, [c_int]),
     "cv_debug_dual_count": (c_int, [c_int]),
     "cv_debug_kernel_log": (c_int, [c_int]),
     "cv_debug_kernel_names": (c_int, [ctypes.c_char_p, c_size_t]),

@@ -546,6 +546,12 @@ int cv_debug_direct_gather_rule(int on);
  * the two launches back to back (the arithmetic of each role is the same); a negative value only queries; returns
  * the previous setting */
 int cv_debug_dual(int on);
+/* test hook: 1 (default) lets the GEMM core take pixel-major tiles where they skip >= 10 % padding work
+ * (cv_gemm_tile.inc), 0 never; a negative value only queries; returns the previous setting (-1: not yet read
+ * from CV_PM) */
+int cv_debug_pm(int on);
+/* test hook: conv contractions planned with pixel-major tiles since the last reset */
+int cv_debug_pm_count(int reset);
 /* test hook: dual grids issued since the last reset */
 int cv_debug_dual_count(int reset);
 /* measurement hook: 1 starts recording (on this thread) the kernels the conv / linear calls launch, clearing the

@@ -198,13 +198,14 @@ def test_conv_fwd_bwd_wgrad(geom, xf, gemm_kernel):
 
 @pytest.mark.parametrize("geom", [g for g in GEOMS if g[2] not in (1, 3)],
                          ids=lambda g: "T" * g[1] + f"{g[2]}x{g[3]}-{g[4]}x{g[5]}k{g[6]}")
-def test_backward_data_stat_epilogue(geom, gemm_kernel):
+def test_backward_data_stat_epilogue(geom, gemm_kernel, batch=16):
     """cv_conv_backward_data with CV_STAT_BWD: the stored tensor is dz = dx * [BN+ReLU active] and the
-    fp64 sums are (sum dz, sum dz*xhat) of the BN layer that feeds this conv."""
+    fp64 sums are (sum dz, sum dz*xhat) of the BN layer that feeds this conv.  (batch: the pixel-major tests
+    call it at batches that are multiples of the tile.)"""
     from cvhip import _lib
 
     n, tr, cin, hin, cout, hout, k, s, p = geom
-    n = 16
+    n = batch
     dev = torch.device("cuda")
     rng = np.random.default_rng(7 + hash(geom) % 1000)
     g = _lib.cv_conv(n, cin, hin, hin, cout, hout, hout, k, k, s, p, tr)
