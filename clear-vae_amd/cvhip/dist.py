@@ -53,8 +53,10 @@ class GradBuckets:
     asynchronously and `wait()` makes the current stream (or, for gloo, the host) wait for every
     launched bucket."""
 
-    def __init__(self, flat: torch.Tensor, bounds: list, group=None):
+    def __init__(self, flat: torch.Tensor, bounds: list, group=None, force: bool = False):
+        """force: issue the collectives even in a world-1 process group (the one-GPU rehearsal of the RCCL path)."""
         self.flat = flat
+        self.force = force
         self.bounds = list(bounds)
         self.views = [flat[lo:hi] for lo, hi in self.bounds]
         self.group = group
@@ -65,7 +67,7 @@ class GradBuckets:
             assert a1 == b0, "buckets must be contiguous and disjoint"
 
     def launch(self, i: int) -> None:
-        if world() > 1 and self.views[i].numel():
+        if (world() > 1 or (self.force and dist.is_available() and dist.is_initialized())) and self.views[i].numel():
             self.pending.append(dist.all_reduce(self.views[i], op=dist.ReduceOp.SUM, group=self.group,
                                                 async_op=True))
 

@@ -52,6 +52,14 @@ from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack
 # strided; MNIST 777k vs 791k img/s, CelebA 99.7k vs 102.3k), so the separate cv_adam_step stays the default
 FUSED_ADAM = os.environ.get("CVHIP_FUSED_ADAM", "0") == "1"  # measured slower (strided Adam RMW): off
 
+# CVHIP_GRAPH_COLLECTIVES=1 (opt-in): a data-parallel step is captured as ONE graph with its RCCL all-reduces inside
+# (issued on the capturing stream: the process group's collective stream joins the capture behind an event edge, the
+# collective's branch runs beside the next backward segment and the Adam segment waits on it), so a step is one
+# graph launch from the host instead of 4 launches + 3 all-reduce calls + 1 wait (CLEAR-MIM: + 5 x (launch,
+# all-reduce, wait, launch)).  Off by default: it needs a backend that supports stream capture (RCCL; not gloo,
+# which the world-2 tests use), and the one-GPU box can only rehearse it at world 1 (tests/test_gpu_graph_collectives.py).
+GRAPH_COLLECTIVES = os.environ.get("CVHIP_GRAPH_COLLECTIVES", "0") == "1"
+
 
 def disc_params(disc):
     """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
@@ -197,6 +205,11 @@ class ClearStep:
         # steps) all advance one stream instead of replaying the same noise from 0
         self.seed, self.offset = rng.offset_tensor(self.device)
         self.world = _dist_world()
+        # the data-parallel programs (segments + buckets); CVHIP_FORCE_DP=1 runs them in a world-1 process group too
+        # (the one-GPU rehearsal of the RCCL paths: a SUM over one rank leaves the gradients as they are)
+        self.dp = self.world > 1 or (os.environ.get("CVHIP_FORCE_DP", "0") == "1" and dist.is_available()
+                                     and dist.is_initialized())
+        self.capture_collectives = GRAPH_COLLECTIVES and self.dp
         if self.world > 1:  # a noise stream per rank (the shards are different samples; equal noise would tie them)
             self.seed = (self.seed ^ (0x9E3779B97F4A7C15 * cvdist.rank())) & 0xFFFFFFFFFFFFFFFF
         self.gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
@@ -215,13 +228,13 @@ class ClearStep:
             self.est_adam = _AdamState(trainer.factor_optimizer, self.est_arena)
             self.learn = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.two_nets = mode in ("mim", "tc")
-        if self.world > 1:  # DDP construction semantics: every rank starts from rank 0's weights
+        if self.dp:  # DDP construction semantics: every rank starts from rank 0's weights
             cvdist.broadcast_flat(self.arena.flat)
             if self.two_nets:
                 cvdist.broadcast_flat(self.est_arena.flat)
-            self.buckets = cvdist.GradBuckets(self.arena.grad, self.bucket_bounds())
+            self.buckets = cvdist.GradBuckets(self.arena.grad, self.bucket_bounds(), force=True)
             if self.two_nets:
-                self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)])
+                self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)], force=True)
         # grads visible through p.grad (like the reference after loss.backward())
         for p in self.arena.params:
             p.grad = self.arena.gview(p)
@@ -331,7 +344,7 @@ class ClearStep:
         # partial tiles, the BN affine gradients and the running statistics are reduced by one
         # cv_step_reduce launch at the end of the backward (data parallel: one per gradient bucket, before
         # the bucket's all-reduce)
-        dp = self.world > 1
+        dp = self.dp
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
         dec = Program()
         ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer)
@@ -468,7 +481,7 @@ class ClearStep:
                     out.append((gp, ap))
                 return out
 
-            if self.world > 1:
+            if self.dp:
                 learn, learn_inj = make_learn_dp(False), make_learn_dp(True)
             else:
                 learn, learn_inj = make_learn(False), make_learn(True)
@@ -490,8 +503,8 @@ class ClearStep:
                 gp.add("cv_tc_learning_step", disc, ws.z, n, tc_work, self.learn, G)
                 ap = Program()
                 ap.add("cv_adam_step", E.flat, E.grad, self.est_adam.m, self.est_adam.v, E.numel,
-                       self.est_adam.hyper, self.est_adam.step, self.gscale if self.world > 1 else None, None)
-                if self.world > 1:
+                       self.est_adam.hyper, self.est_adam.step, self.gscale if self.dp else None, None)
+                if self.dp:
                     return [(gp, ap)]
                 gp.extend(ap)
                 return gp
@@ -538,7 +551,7 @@ class ClearStep:
         fwd = G["fwd_inj" if inject else "fwd"]
         lat = G["lat_inj" if inject else "lat"]
         learn = G["learn_inj" if inject else "learn"]
-        if self.world == 1:
+        if not self.dp:
             progs = [fwd, G["dec"], lat, G["enc"], G["upd"]] + ([learn] if learn is not None else [])
             return [("prog", progs)]
         seg = [("prog", [fwd, G["dec"]]), ("ar", 0), ("prog", [lat, G["enc"]]), ("ar", 1), ("prog", [G["enc2"]]),
@@ -609,7 +622,27 @@ class ClearStep:
 
     def _capture(self, G):
         """One executable HIP graph per program segment (_lib.StepGraph: launched directly, without
-        PyTorch's per-replay RNG bookkeeping)."""
+        PyTorch's per-replay RNG bookkeeping); with capture_collectives, one graph for the whole data-parallel step,
+        its all-reduces captured between the segments (the first, eager step has created the communicators)."""
+        if self.capture_collectives:
+            def record_all(s, segs=self._segments(G, False)):
+                for item in segs:
+                    kind = item[0]
+                    if kind == "prog":
+                        for P in item[1]:
+                            P.run(s)
+                    elif kind == "ar":
+                        self.buckets.launch(item[1])
+                    elif kind == "wait":
+                        self.buckets.wait()
+                    elif kind == "ar_est":
+                        self.est_buckets.launch(0)
+                    elif kind == "wait_est":
+                        self.est_buckets.wait()
+
+            G["graphs"] = [_lib.StepGraph(record_all)]
+            G["one_graph"] = True
+            return
         graphs = []
         for item in self._segments(G, False):
             if item[0] != "prog":
@@ -642,7 +675,7 @@ class ClearStep:
         all-reduced under DP — and before the Adam launch; such a step runs eagerly, not from the graph (used by
         the tests to read the step's activations with the pre-update parameters)."""
         n = X.shape[0]
-        if before_update is not None and FUSED_ADAM and self.world == 1:
+        if before_update is not None and FUSED_ADAM and not self.dp:
             # (Adam rides in the reduction launch of the `enc` program: there is no point between the complete
             # gradients and the update at which the hook could run)
             raise RuntimeError("before_update is not supported with CVHIP_FUSED_ADAM=1")
@@ -659,7 +692,9 @@ class ClearStep:
         use_graph = G["count"] >= 1 and not inject and self.graphs_enabled and before_update is None
         if use_graph and "graphs" not in G:
             self._capture(G)
-        if use_graph:
+        if use_graph and G.get("one_graph"):
+            G["graphs"][0].replay()  # (the whole step, collectives included: one launch)
+        elif use_graph:
             self._run_segments(self._segments(G, False), G["graphs"])
         else:
             self._run_eager(G, inject, before_update)

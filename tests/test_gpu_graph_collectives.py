@@ -1,0 +1,56 @@
+"""CVHIP_GRAPH_COLLECTIVES=1 (cvhip/engine.py): the data-parallel step captured as ONE graph with its RCCL
+all-reduces inside, rehearsed on the one-GPU box in a world-1 `nccl` process group (tests/graph_coll_worker.py,
+CVHIP_FORCE_DP=1 so the buckets really go through RCCL).  Reference step: /root/reference/code/src/trainer.py:861-888
+(the VAE backward + Adam, then CLEAR-MIM's 5 estimator updates, each with its own gradient all-reduce under DDP).
+
+For CLEAR and CLEAR-MIM, 4 steps (one eager, three replayed) run with the captured form and with the
+host-sequenced segments (graphs between host-issued all-reduces, the default):
+  * the captured form really built one graph for the step (and the default one per segment);
+  * losses of every step and the final parameter / Adam-state arenas agree to 1e-5 relative between the two (the
+    same kernels in the same order; a SUM over one rank leaves the gradients as they are; two runs of the step are
+    not bitwise reproducible — the decoder-input backward's dz partials are fp32 atomics — so a run-to-run floor
+    of ~1e-7 remains; an Adam launch racing its gradients, or a replay skipping a segment, would be off by far
+    more).
+The 2- to 8-rank RCCL runs are the driver's: a one-GPU box cannot hold two RCCL ranks."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(mode, captured):
+    env = dict(os.environ, CVHIP_FORCE_DP="1", CVHIP_GRAPH_COLLECTIVES="1" if captured else "0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "graph_coll_worker.py"), mode, "4",
+                        str(_free_port())], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("mode", ["clear", "mim"])
+def test_captured_collectives_match_host_sequenced(mode):
+    a = _run(mode, True)
+    b = _run(mode, False)
+    assert a["capture"] and a["one_graph"] and a["ngraphs"] == 1, a
+    assert not b["capture"] and not b["one_graph"] and b["ngraphs"] > 1, b
+    def close(u, v, tol=1e-5):
+        return abs(u - v) <= tol * max(abs(v), 1e-3)
+
+    for sa, sb in zip(a["losses"], b["losses"]):
+        assert len(sa) == len(sb) and all(close(u, v) for u, v in zip(sa, sb)), (sa, sb)
+    for k in b["digest"]:
+        assert close(a["digest"][k], b["digest"][k], 1e-6), (k, a["digest"][k], b["digest"][k])
+    assert all(close(u, v) for u, v in zip(a["flat_head"], b["flat_head"])), (a["flat_head"], b["flat_head"])
