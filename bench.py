@@ -179,6 +179,8 @@ def isolated_pass(G, reps=20, rounds=3):
     times = {}
     for pname, P in _programs(G):
         for i, (name, fn, args, _lane) in enumerate(P.calls):
+            if fn is None:  # (a stream join, no launch)
+                continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 s = _lib.stream_handle()

@@ -128,6 +128,7 @@ struct CombineArgs {
   const double* rec_in;
   float* dheads;
   float* losses;
+  int accumulate;  // 1: dheads += (the contrastive / MI terms are already in it)
 };
 
 template <int NTH>
@@ -171,9 +172,12 @@ __device__ __forceinline__ void combine_body(const CombineArgs& C, double* scrat
       const float el = expf(l[q]);
       const double term = (double)(1.0f + l[q] - m[q] * m[q] - el);
       if (j < d) sc += term; else ss += term;
-      dheads[(size_t)r * 4 * d + blk * d + k] = w * m[q] * inv_n + g[q];
-      dheads[(size_t)r * 4 * d + (blk + 1) * d + k] =
-          w * (-0.5f * inv_n) * (1.0f - el) + g[q] * (zz[q] - m[q]) * 0.5f;
+      const float vm = w * m[q] * inv_n + g[q];
+      const float vl = w * (-0.5f * inv_n) * (1.0f - el) + g[q] * (zz[q] - m[q]) * 0.5f;
+      float* pm = dheads + (size_t)r * 4 * d + blk * d + k;
+      float* pl = dheads + (size_t)r * 4 * d + (blk + 1) * d + k;
+      *pm = C.accumulate ? *pm + vm : vm;
+      *pl = C.accumulate ? *pl + vl : vl;
     }
   }
   const double kc = block_sum<NTH>(sc, scratch);
@@ -1205,9 +1209,20 @@ extern "C" int cv_latent_combine(const float* heads, const float* z, const float
                                  float* dheads, float* losses, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine: bad args");
-  const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses};
+  const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 0};
   hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), C);
   CV_LAUNCH_CHECK("latent_combine");
+  return 0;
+}
+
+extern "C" int cv_latent_combine_acc(const float* heads, const float* z, const float* dz, int n, int d, float beta,
+                                     float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                                     float* dheads, float* losses, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine_acc: bad args");
+  const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 1};
+  hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), C);
+  CV_LAUNCH_CHECK("latent_combine_acc");
   return 0;
 }
 
@@ -1289,7 +1304,7 @@ extern "C" int cv_latent_step(const float* heads, const float* z, const float* d
     CV_REQUIRE(br[i].dmu == nullptr || (br[i].dmu >= dheads && br[i].dmu < dheads + (size_t)n * 4 * d),
                "latent_step: branch %d gradient must land in dheads", i);
   a.with_combine = 1;
-  a.cmb = CombineArgs{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses};
+  a.cmb = CombineArgs{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 0};
   // one launch when its grid is resident at once (ntxent_fused_kernel), else launch 1: row log-sum-exps of every
   // branch + the KL / decoder-chain seed of dheads (independent); launch 2: contrastive losses and their gradients
   // accumulated into dheads

@@ -266,6 +266,11 @@ _SIGS = {
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p],
     ),
+    "cv_latent_combine_acc": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p],
+    ),
     "cv_mse_sum": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cv_ntxent": (
         c_int,

@@ -60,6 +60,17 @@ FUSED_ADAM = os.environ.get("CVHIP_FUSED_ADAM", "0") == "1"  # measured slower (
 # which the world-2 tests use), and the one-GPU box can only rehearse it at world 1 (tests/test_gpu_graph_collectives.py).
 GRAPH_COLLECTIVES = os.environ.get("CVHIP_GRAPH_COLLECTIVES", "0") == "1"
 
+# CVHIP_LATENT_SIDE=1 (A/B knob, off: measured slower): the NT-Xent terms depend only on the heads, so their two launches (row
+# log-sum-exps, then the gradients, accumulated into a d(heads) the step's first launch zeroed) fork onto a side
+# stream right after the heads launch and run beside the decoder forward / backward; the step joins them before the
+# KL / decoder-chain seed (cv_latent_combine_acc), which now adds onto them.  The same two adds per element, in the
+# other order: d(heads) is bit-identical.  Single-graph steps only (a data-parallel step captured per segment would
+# leave the fork unjoined in its first graph).  Measured (round 5, same box, 2 rounds): MNIST 0.5155 -> 0.5241 ms,
+# C3 4.236 -> 4.276 ms — the graph's fork / join edges cost more than the 31 us of NT-Xent they take off the
+# critical path, as for the side-stream weight gradients; so the two launches stay on the critical
+# path (cv_latent_step).
+LATENT_SIDE = os.environ.get("CVHIP_LATENT_SIDE", "0") == "1"
+
 
 def disc_params(disc):
     """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
@@ -318,15 +329,42 @@ class ClearStep:
                                 device=self.device)
             gscale_rec = torch.ones(1, dtype=torch.float32, device=self.device)
 
+        # the contrastive branches (trainer.py:474-479): [mu_c, logvar_c] and [mu_s, logvar_s] of the heads, their
+        # gradients into d(heads)
+        hb = ws.heads.data_ptr()
+        dh = ws.dheads.data_ptr()
+        branches = None
+        if not grouped:
+            alpha = float(hp["alpha"])
+            tau = float(hp["temperature"])
+            branches = [cv_ntxent_branch(hb, hb + 4 * d, 4 * d, 0, dh, dh + 4 * d, 4 * d, None, alpha,
+                                         ws.losses.data_ptr() + 12, ws.lse[0].data_ptr())]
+        if self.mode == "clear":
+            ps = bool(hp["ps"])
+            branches.append(cv_ntxent_branch(hb + 8 * d, hb + 12 * d, 4 * d, int(ps), dh + 8 * d, dh + 12 * d, 4 * d,
+                                             None, alpha if ps else -alpha, ws.losses.data_ptr() + 16,
+                                             ws.lse[1].data_ptr()))
+        br_arr = (cv_ntxent_branch * len(branches))(*branches) if branches is not None else None
+        # NT-Xent beside the decoder (LATENT_SIDE): CLEAR / CLEAR-MIM steps captured as one graph
+        side_nt = (LATENT_SIDE and br_arr is not None and self.mode in ("clear", "mim")
+                   and (not self.dp or self.capture_collectives))
+
         def make_fwd(inject: bool):
             f = Program()
             # one launch refreshes the packed conv weights and zeroes the BN sums, the gradient arena and the
-            # two split-K / accumulated latent buffers of the step
+            # two split-K / accumulated latent buffers of the step (and d(heads) when the NT-Xent gradients
+            # accumulate into it from the side stream)
             bufs = [(ws.stats, ws.stats.numel() * 8), (A.grad, A.numel * 4), (ws.heads, ws.heads.numel() * 4),
                     (ws.dz, ws.dz.numel() * 4)]
+            if side_nt:
+                bufs.append((ws.dheads, ws.dheads.numel() * 4))
             pack_program(sp, f, "all", zero=bufs)
             rp = None if grouped else (eps_buf[0] if inject else None, self.seed, self.offset)
             drew = ws.encoder_program(f, X, True, zero_heads=False, reparam=rp)
+            if side_nt:  # row log-sum-exps + gradients of both branches on the side stream (joined in `lat`)
+                f.add_fork("cv_ntxent", br_arr, len(branches), lab, n, d, self.sim, ctypes.c_float(tau), 2, 1)
+                f.keep.append(br_arr)
+                f.join_at_end = False
             if grouped:
                 hb = ws.heads.data_ptr()
                 f.add("cv_group_forward", self.group_mode, hb, hb + 4 * d, 4 * d, lab, n, d, gwork, gscale_rec,
@@ -353,27 +391,22 @@ class ClearStep:
 
         # latent terms -> d(heads)
         lat = Program()
-        hb = ws.heads.data_ptr()
-        dh = ws.dheads.data_ptr()
         if grouped:
             lat.add("cv_group_backward", self.group_mode, ws.heads, ws.z, ws.dz, gwork, n, d,
                     ctypes.c_float(float(hp["beta"])), ctypes.c_float(float(hp.get("loc", 0))),
                     ctypes.c_float(float(hp.get("scale", 1))), self.anneal, ws.rec, ws.dheads, ws.losses)
             lat_inj = lat
             lat.keep.append(gwork)
-            branches = None
-        else:
-            alpha = float(hp["alpha"])
-            tau = float(hp["temperature"])
-            branches = [cv_ntxent_branch(hb, hb + 4 * d, 4 * d, 0, dh, dh + 4 * d, 4 * d, None, alpha,
-                                         ws.losses.data_ptr() + 12, ws.lse[0].data_ptr())]
-        if self.mode == "clear":
-            ps = bool(hp["ps"])
-            branches.append(cv_ntxent_branch(hb + 8 * d, hb + 12 * d, 4 * d, int(ps), dh + 8 * d, dh + 12 * d, 4 * d,
-                                             None, alpha if ps else -alpha, ws.losses.data_ptr() + 16,
-                                             ws.lse[1].data_ptr()))
-        if branches is not None:
-            arr = (cv_ntxent_branch * len(branches))(*branches)
+        elif side_nt:
+            # join the NT-Xent side stream, then the KL + decoder-chain seed added onto its gradients
+            lat.add_join()
+            lat.add("cv_latent_combine_acc", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
+                    ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
+                    ws.rec, ws.dheads, ws.losses)
+            lat_inj = Program()
+            lat_inj.extend(lat)
+        if branches is not None and not side_nt:
+            arr = br_arr
             # KL + decoder chain into d(heads) with the contrastive terms accumulated on top
             lat.add("cv_latent_step", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
                     ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,

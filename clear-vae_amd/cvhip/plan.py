@@ -455,6 +455,15 @@ class Program:
     def add_side(self, name: str, *args):
         self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1 if SIDE_STREAM else 0))
 
+    def add_fork(self, name: str, *args):
+        """A call on the side stream regardless of CVHIP_SIDE_STREAM (it forks from the main-stream calls before
+        it; a later add_join, in this or a later program, joins it back)."""
+        self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1))
+
+    def add_join(self):
+        """The main stream waits here for everything issued on the side stream so far."""
+        self.calls.append(("join", None, [], 2))
+
     def extend(self, other: "Program"):
         self.calls += other.calls
         self.keep += other.keep
@@ -480,11 +489,18 @@ class Program:
             return
         side = _side_stream(main.device)
         if self._events is None:  # created on the first (eager) run, reused by graph capture
-            nf = sum(1 for i, c in enumerate(self.calls) if c[3] and (i == 0 or not self.calls[i - 1][3]))
-            self._events = [torch.cuda.Event() for _ in range(nf + 1)]
+            nf = sum(1 for i, c in enumerate(self.calls) if c[3] == 1 and (i == 0 or self.calls[i - 1][3] != 1))
+            nj = sum(1 for c in self.calls if c[3] == 2)
+            self._events = [torch.cuda.Event() for _ in range(nf + nj + 1)]
         ev = 0
         prev_lane = 0
         for i, (name, fn, args, lane) in enumerate(self.calls):
+            if lane == 2:  # explicit join: the main stream waits for the side stream's work so far
+                self._events[ev].record(side)
+                main.wait_event(self._events[ev])
+                ev += 1
+                prev_lane = 0
+                continue
             if lane and not prev_lane:  # fork: the side stream waits for the main-stream work so far
                 self._events[ev].record(main)
                 side.wait_event(self._events[ev])

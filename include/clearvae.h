@@ -339,6 +339,12 @@ int cv_kl(const float* mu, const float* logvar, int ld, int n, int d, float* kl_
 int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                       float loc, float scale, const int64_t* anneal_step, const double* rec_in,
                       float* dheads, float* losses, cv_stream_t stream);
+/* cv_latent_combine with dheads += instead of overwritten: the fused step whose NT-Xent gradients were already
+ * accumulated into a zeroed dheads (their launches run on a side stream during the decoder pass, and the step
+ * joins it before this call; cvhip/engine.py LATENT_SIDE). */
+int cv_latent_combine_acc(const float* heads, const float* z, const float* dz, int n, int d, float beta,
+                          float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                          float* dheads, float* losses, cv_stream_t stream);
 
 /* reconstruction term (losses.py:45-47) for the autograd path: rec = mean_n sum (xhat - x)^2;
  * work: one zeroed fp64 word.  dxhat != NULL: dxhat = gscale[0] * 2 (xhat - x) / n. */
