@@ -69,6 +69,9 @@ CONFIGS = {
     # 128 per GPU, bf16 contractions
     "camelyon-bf16": ("VAE64", 64, 3, 64, 128, "clear", 2,
                       dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, ps=True, precision="bf16"), None),
+    # the same shard in fp32: the bf16 speed-up is measured in the same run (key camelyon_fp32, N = 1 only)
+    "camelyon-fp32": ("VAE64", 64, 3, 64, 128, "clear", 2,
+                      dict(beta=1 / 32, vae_lr=3e-5, alpha=100.0, temperature=0.1, ps=True), None),
 }
 
 
@@ -179,7 +182,7 @@ def isolated_pass(G, reps=20, rounds=3):
     times = {}
     for pname, P in _programs(G):
         for i, (name, fn, args, _lane) in enumerate(P.calls):
-            if fn is None:  # (a stream join, no launch)
+            if fn is None or name in ("cv_ntxent_aux", "cv_ntxent_aux_flush"):  # (a join; a queue / its flush)
                 continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -777,6 +780,11 @@ def main():
             assert ccfg[4] == bs, (cname, ccfg[4])
             scaling[key] = scaling_entry(cname, ccfg, min(args.steps, 100), device, world, rank,
                                          detail=not args.no_kernel_pass)
+        if world == 1:  # (configs[4]'s shard in fp32 beside the bf16 key: their ratio is the bf16 speed-up)
+            scaling["camelyon_fp32"] = scaling_entry("camelyon-fp32", CONFIGS["camelyon-fp32"], min(args.steps, 100),
+                                                     device, world, rank, detail=False)
+            scaling["camelyon_bf16"]["speedup_vs_fp32"] = round(scaling["camelyon_bf16"]["value"]
+                                                                / scaling["camelyon_fp32"]["value"], 4)
     if rank == 0:
         rec = {
             "metric": "training images/sec at bs=512; ELBO rel-err vs CPU ref",

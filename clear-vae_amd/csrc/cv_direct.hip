@@ -41,6 +41,10 @@
 #include "cv_direct.hpp"
 
 namespace cv {
+int direct_aux_launch(const int* dkey, const direct::DArgs& da, dim3 dgrid, size_t dlds, hipStream_t st);
+}  // namespace cv
+
+namespace cv {
 namespace direct {
 
 template <int OP, int XA, int EPI, int CBT, int FMX>
@@ -310,6 +314,14 @@ static int direct_run(int op, const Geo& g, const cv_operand* in, const float* w
     c.kern = kern;
     ++g_direct_launches;
     return 0;
+  }
+  {  // a queued NT-Xent phase rides in this grid (cv_aux.hip) where the pair is served
+    const int key[5] = {op, in->xf, epi, cbt, fmx <= 1 ? 1 : (fmx <= 2 ? 2 : 4)};
+    const int ar = direct_aux_launch(key, a, grid, lds, st);
+    if (ar >= 0) {
+      ++g_direct_launches;
+      return ar;
+    }
   }
   void* params[] = {&a};
   note_launch(kern);

@@ -1231,7 +1231,8 @@ struct WPlan {
 // the workgroups (MNIST decoder convT1 gradient 37.2 -> 35.0 us, VAE64 conv5 pair 200.6 -> 195.3 us; applied
 // everywhere they cost VAE64's 1024-workgroup gradients ~7 us each).
 // cap_ovr >= 0 replaces the dual-capture row cap (the workspace query takes the max over both choices).
-static WPlan wgrad_plan(int M, int N, long K, int split_k, int cap_ovr = -1) {
+// tgt_ovr > 0 replaces the workgroup target (pixel-major launches: wgrad_pm_target).
+static WPlan wgrad_plan(int M, int N, long K, int split_k, int cap_ovr = -1, long tgt_ovr = 0) {
   WPlan w;
   const int Ntot = N + 1;
   w.BN = (Ntot <= 16) ? 16 : (Ntot <= 32) ? 32 : 64;
@@ -1248,7 +1249,8 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k, int cap_ovr = -1) {
   auto split_for = [&](int bm) -> long {
     if (split_k > 0) return split_k > 4096 ? 4096 : split_k;
     const long tiles = (long)cdiv(M, bm) * cdiv(Ntot, w.BN);
-    long split = (target + tiles - 1) / tiles;
+    const long tg = tgt_ovr > 0 ? tgt_ovr : target;
+    long split = (tg + tiles - 1) / tiles;
     long maxs = ktiles / 8;
     if (tiles * maxs < 256) maxs = ktiles / 4;
     if (maxs < 1) maxs = 1;
@@ -1277,13 +1279,32 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k, int cap_ovr = -1) {
 
 // Queried outside any capture, so it must cover both row tiles a launch may take: the plain plan and the one capped
 // at 64 rows inside a dual grid (today the capped split never exceeds the uncapped one, but nothing forces that).
+// Workgroups a pixel-major WGRAD launch aims for.  Its tiles walk only the pixels their tap reads inside the image, so
+// they are shorter than the plain plan assumes; where 64-row tiles alone give >= 256 workgroups (VAE64's conv5 and
+// convT1 gradients: 512 tiles) the launch takes no K split at all — every tile writes its gradient block once, no
+// split-K partials for cv_step_reduce (C3's conv5 pair 189.9 -> 160.3 us in-step); below that (conv4 / convT2: 128
+// tiles) the plain target's split stays (256 there measured the pair 168 -> 187 us).  CV_PM_WTARGET: a fixed target
+// (A/B).
+static long wgrad_pm_target(long tiles64 = 0) {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_PM_WTARGET");
+    v = e ? atol(e) : 0;
+    if (v < 0) v = 0;
+  }
+  if (v > 0) return v;
+  return tiles64 >= 256 ? tiles64 : 0;
+}
+
 static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
   size_t b = 0;
-  for (int cap : {0, 64}) {
-    const WPlan w = wgrad_plan(M, N, K, split_k, cap);
-    const size_t need = w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
-    if (need > b) b = need;
-  }
+  const long t64 = (long)cdiv(M, 64) * cdiv(N + 1, (N + 1 <= 16) ? 16 : (N + 1 <= 32) ? 32 : 64);
+  for (int cap : {0, 64})
+    for (long tg : {0L, wgrad_pm_target(t64)}) {
+      const WPlan w = wgrad_plan(M, N, K, split_k, cap, tg);
+      const size_t need = w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
+      if (need > b) b = need;
+    }
   return b;
 }
 
@@ -1349,6 +1370,13 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   a.K = g.n * g.hs * g.ws;
   WPlan w = wgrad_plan(a.M, a.N, a.K, split_k);
   const int Ntot = a.N + (gbias ? 1 : 0);
+  // pixel-major K (a K tile = 32 images at one small pixel; an N tile = one tap): the tile skips the pixels at which
+  // its tap reads padding (the split is then re-cut per tile over the pixels it visits)
+  a.pm = (!gbias && g.cb % w.BN == 0 && g.hs * g.ws <= 16 && pm_pays(g, BK)) ? 1 : 0;
+  if (a.pm && split_k <= 0) {
+    const long tg = wgrad_pm_target((long)cdiv(a.M, 64) * cdiv(Ntot, w.BN));
+    if (tg > 0) w = wgrad_plan(a.M, a.N, a.K, split_k, -1, tg);
+  }
   if (split_k <= 0 && w.split > 1) {
     // one round of resident workgroups: a second, partial round costs a whole extra workgroup time
     // (prologue + K loop + epilogue) while fewer, longer splits only lengthen the K loop
@@ -1364,9 +1392,6 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
     }
   }
   a.kchunk = w.kchunk;
-  // pixel-major K (a K tile = 32 images at one small pixel; an N tile = one tap): the tile skips the pixels at which
-  // its tap reads padding (the split is then re-cut per tile over the pixels it visits)
-  a.pm = (!gbias && g.cb % w.BN == 0 && g.hs * g.ws <= 16 && pm_pays(g, BK)) ? 1 : 0;
   static int atomic_splits = -1;  // A/B knob CV_WGRAD_ATOMIC=1: split-K tiles added with fp32 atomics, no partials
   if (atomic_splits < 0) {
     const char* e = getenv("CV_WGRAD_ATOMIC");

@@ -266,6 +266,11 @@ _SIGS = {
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p],
     ),
+    "cv_ntxent_aux": (
+        c_int,
+        [_P(cv_ntxent_branch), c_int, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
+    ),
+    "cv_ntxent_aux_flush": (c_int, [c_void_p]),
     "cv_latent_combine_acc": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
@@ -347,6 +352,8 @@ _SIGS = {
     "cv_debug_direct_gather_rule": (c_int, [c_int]),
     "cv_debug_dual": (c_int, [c_int]),
     "cv_debug_pm": (c_int, [c_int]),
+    "cv_debug_aux": (c_int, [c_int]),
+    "cv_debug_aux_count": (c_int, [c_int]),
     "cv_debug_pm_count": (c_int, [c_int]),
     "cv_debug_dual_count": (c_int, [c_int]),
     "cv_debug_kernel_log": (c_int, [c_int]),

@@ -71,6 +71,14 @@ GRAPH_COLLECTIVES = os.environ.get("CVHIP_GRAPH_COLLECTIVES", "0") == "1"
 # path (cv_latent_step).
 LATENT_SIDE = os.environ.get("CVHIP_LATENT_SIDE", "0") == "1"
 
+# CVHIP_LATENT_AUX (default 1): the NT-Xent phases queued into the decoder forward instead (cv_ntxent_aux): the row
+# log-sum-exps ride in the first decoder ConvTranspose2d's grid, the losses and gradients (accumulated into the
+# zeroed d(heads)) in the second's, as extra workgroups of the same launch where the library serves the pair
+# (cv_aux.hip), else as their own launches at those points; the KL / decoder-chain seed adds onto them after the
+# decoder backward (cv_latent_combine_acc).  One stream, no graph edges; d(heads) is bit-identical (the same two adds
+# per element, in the other order).
+LATENT_AUX = os.environ.get("CVHIP_LATENT_AUX", "1") == "1"
+
 
 def disc_params(disc):
     """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
@@ -348,6 +356,11 @@ class ClearStep:
         # NT-Xent beside the decoder (LATENT_SIDE): CLEAR / CLEAR-MIM steps captured as one graph
         side_nt = (LATENT_SIDE and br_arr is not None and self.mode in ("clear", "mim")
                    and (not self.dp or self.capture_collectives))
+        aux_nt = (not side_nt and LATENT_AUX and br_arr is not None and self.mode in ("clear", "mim")
+                  and len(sp.dec) >= 3)
+        tau_c = ctypes.c_float(float(hp["temperature"])) if br_arr is not None else None
+        aux_args = ([(br_arr, len(branches), lab, n, d, self.sim, tau_c, ph, 1) for ph in (0, 1)]
+                    if aux_nt else None)
 
         def make_fwd(inject: bool):
             f = Program()
@@ -356,7 +369,7 @@ class ClearStep:
             # accumulate into it from the side stream)
             bufs = [(ws.stats, ws.stats.numel() * 8), (A.grad, A.numel * 4), (ws.heads, ws.heads.numel() * 4),
                     (ws.dz, ws.dz.numel() * 4)]
-            if side_nt:
+            if side_nt or aux_nt:
                 bufs.append((ws.dheads, ws.dheads.numel() * 4))
             pack_program(sp, f, "all", zero=bufs)
             rp = None if grouped else (eps_buf[0] if inject else None, self.seed, self.offset)
@@ -373,7 +386,9 @@ class ClearStep:
                 ws.decoder_program(f, ws.z, True, "loss", X, rec_scale=gscale_rec)
                 f.keep += [gwork, gscale_rec]
             else:
-                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp)
+                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp, aux=aux_args)
+                if aux_nt:
+                    f.keep.append(br_arr)
             # (the running statistics are folded at the end of the backward by cv_step_reduce)
             return f
 
@@ -397,15 +412,16 @@ class ClearStep:
                     ctypes.c_float(float(hp.get("scale", 1))), self.anneal, ws.rec, ws.dheads, ws.losses)
             lat_inj = lat
             lat.keep.append(gwork)
-        elif side_nt:
-            # join the NT-Xent side stream, then the KL + decoder-chain seed added onto its gradients
-            lat.add_join()
+        elif side_nt or aux_nt:
+            # (side stream: join it first) the KL + decoder-chain seed added onto the NT-Xent gradients
+            if side_nt:
+                lat.add_join()
             lat.add("cv_latent_combine_acc", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
                     ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
                     ws.rec, ws.dheads, ws.losses)
             lat_inj = Program()
             lat_inj.extend(lat)
-        if branches is not None and not side_nt:
+        if branches is not None and not side_nt and not aux_nt:
             arr = br_arr
             # KL + decoder chain into d(heads) with the contrastive terms accumulated on top
             lat.add("cv_latent_step", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),

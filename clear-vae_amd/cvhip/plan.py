@@ -782,9 +782,11 @@ class Workspace:
         C, Hh, Wh = sp.feat
         return self.FUSED_HEADS and bool(_lib.lib().cv_heads_backward_supported(self.n, sp.F, C, 4 * sp.d))
 
-    def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None):
+    def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None,
+                        aux=None):
         """reparam = (eps, seed, offset): z is drawn from self.heads first (cv_reparam_forward, or inside the
-        fused decoder-input launch); None: z is given."""
+        fused decoder-input launch); None: z is given.  aux: cv_ntxent_aux argument tuples, the i-th queued before
+        the i-th decoder conv (its phase rides in that launch where served) and flushed right after it."""
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
@@ -817,7 +819,11 @@ class Workspace:
                 P.add("cv_convt_output_loss", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep, self.bn_dec[-1].cv(True), x,
                       self.xhat, self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
                 return
+            if aux is not None and li < len(aux):
+                P.add("cv_ntxent_aux", *aux[li])
             P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, self.y_dec[li], ep)
+            if aux is not None and li < len(aux):
+                P.add("cv_ntxent_aux_flush")
             cur = self.y_dec[li]
         if output == "xhat":
             P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)

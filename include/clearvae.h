@@ -366,6 +366,16 @@ typedef struct cv_ntxent_branch {
 } cv_ntxent_branch;
 int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim,
               float temperature, int phase, int accumulate, cv_stream_t stream);
+/* An NT-Xent phase of cv_ntxent (phase 0: the row log-sum-exps; 1: the losses and gradients, accumulated into the
+ * branches' d(mu) / d(logvar) when accumulate) queued to run as extra workgroups of this thread's next direct-kernel
+ * conv launch on `stream`'s order (cv_aux.hip: MNIST's decoder ConvTranspose2d forwards serve it); the call after
+ * that conv must be cv_ntxent_aux_flush, which launches the phase on its own if no launch took it.  One phase at
+ * a time (a phase still queued when the next is queued is launched first, on `stream`); the phases read only the
+ * heads and labels (trainer.py:474-479, losses.py:98-137), so the fused step
+ * queues them into its decoder forward.  The branch gradients must not be read before the flush. */
+int cv_ntxent_aux(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim, float temperature,
+                  int phase, int accumulate, cv_stream_t stream);
+int cv_ntxent_aux_flush(cv_stream_t stream);
 
 /* The fused step's latent terms in two launches (trainer.py:452-480): cv_latent_combine (KL with the
  * annealer weight, the decoder gradient chained through z) and cv_ntxent phase 2 with accumulate = 1
@@ -558,6 +568,11 @@ int cv_debug_dual(int on);
 int cv_debug_pm(int on);
 /* test hook: conv contractions planned with pixel-major tiles since the last reset */
 int cv_debug_pm_count(int reset);
+/* test hook: 1 (default) lets a queued NT-Xent phase ride in a served direct launch (cv_ntxent_aux), 0 launches it
+ * on its own at the flush; a negative value only queries; returns the previous setting */
+int cv_debug_aux(int on);
+/* test hook: direct + NT-Xent grids issued since the last reset */
+int cv_debug_aux_count(int reset);
 /* test hook: dual grids issued since the last reset */
 int cv_debug_dual_count(int reset);
 /* measurement hook: 1 starts recording (on this thread) the kernels the conv / linear calls launch, clearing the
