@@ -466,6 +466,19 @@ __global__ __launch_bounds__(ET, 3) void edge_gather_kernel(const EArgs P) {
 // grid is resident at once; the wait is bounded, a timeout sets g_eo_sync[3] and proceeds), folds the output
 // BN's constants and turns its band — still in LDS — into x_hat, the reconstruction sum and dv, with the
 // arithmetic of output_loss_kernel.  The last workgroup out resets the counters.
+// One-channel image (CB = 1: MNIST's decoder output): only 4 of the 16 MFMA columns would carry a class, so the
+// contraction runs on v_mfma_f32_4x4x1f32 instead, A (the 4 classes' weights, from lanes 0..3) broadcast to the 16
+// blocks and B = one staged small-grid value per lane: lane l accumulates all four classes of image block l of a
+// 64-block tile (4x fewer MFMA cycles per block than the 16-column tile).  The weights stay in LDS, [class][q*32 + ch]
+// at pitch WKP4, behind the output tile, followed by one zero pixel that out-of-image neighbours read.
+constexpr int WKP4 = 4 * CS + 4;
+__host__ __device__ constexpr int m4_off(int ipb, int ws, int rb, int wb) {
+  const int e = ipb * ws * SP + 2 * rb * wb;  // staged rows + the output tile (CB = 1)
+  const int lo = 4 * ET * (int)(sizeof(double) / sizeof(float));  // (clear of the BN fold scratch: 4 ET doubles)
+  return ((e > lo ? e : lo) + 3) & ~3;
+}
+constexpr int M4_EXTRA = 4 * WKP4 + SP;  // floats
+
 struct OArgs {
   cv_bn bn;               // the output BatchNorm2d (this launch's statistics epilogue fills its sums)
   const float* x;         // [n][CB][hb][wb] the input batch (NCHW)
@@ -477,7 +490,7 @@ struct OArgs {
 };
 __device__ unsigned g_eo_sync[4];  // [0] arrivals, [1] finishes, [3] timeout flag
 
-template <int CB, int KK, bool OUT>
+template <int CB, int KK, bool OUT, bool M4 = CB == 1>
 __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EArgs P, const OArgs O) {
   constexpr int NCOL = 4 * CB;  // GEMM columns: class (2 cy + cx) * CB + output channel
   static_assert(NCOL <= 16 && KK <= 4, "one 16-column tile; taps cy + 2 - 2 dy < 4");
@@ -503,9 +516,30 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   // [tap][cs][cb] (coalesced reads of the KK*KK*32*CB weights), pitch WKP: the 16 lanes of a b128 read hit
   // 16 disjoint 4-bank groups
   constexpr int WKP = 4 * CS + 4;
+  static_assert(!M4 || CB == 1, "the 4x4x1 form serves one output channel");
+  float* sW4 = sIn + m4_off(P.ipb, g.ws, P.rows, g.wb);  // (M4) [4][WKP4], then the zero pixel
+  float* sZ = sW4 + 4 * WKP4;
   // the block-matrix weights: all 8 per thread in flight
-  float* sWb = sIn + 4 * ET * 2;  // [16][WKP] behind the fold scratch, inside the (not yet used) staging area
-  {
+  float* sWb = M4 ? sW4 : sIn + 4 * ET * 2;  // [16][WKP] behind the fold scratch, inside the (not yet used) staging area
+  if constexpr (M4) {
+    constexpr int NW4 = 4 * 4 * CS / ET;
+    static_assert(NW4 * ET == 4 * 4 * CS, "class weights: whole rounds of ET");
+    float wv[NW4];
+#pragma unroll
+    for (int r = 0; r < NW4; ++r) {
+      const int i = t + r * ET;
+      const int c2 = i / (4 * CS), k = i - c2 * (4 * CS), q = k / CS, ch = k - q * CS;
+      const int kh = (c2 >> 1) + 2 - 2 * (q >> 1), kw = (c2 & 1) + 2 - 2 * (q & 1);
+      wv[r] = (kh < KK && kw < KK) ? P.w[(kh * KK + kw) * CS + ch] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NW4; ++r) {
+      const int i = t + r * ET;
+      const int c2 = i / (4 * CS), k = i - c2 * (4 * CS);
+      sW4[c2 * WKP4 + k] = wv[r];
+    }
+    if (t < SP) sZ[t] = 0.f;
+  } else {
     constexpr int NWB = 16 * 4 * CS / ET;
     static_assert(NWB * ET == 16 * 4 * CS, "block matrix: whole rounds of ET");
     float wv[NWB];
@@ -530,16 +564,18 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   __syncthreads();
   CV_ESTAMP(st1);
   float bw[4][8];
+  if constexpr (!M4) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 w0 = lds4(sWb + nl * WKP + q * CS + 8 * kq), w1 = lds4(sWb + nl * WKP + q * CS + 8 * kq + 4);
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w0 = lds4(sWb + nl * WKP + q * CS + 8 * kq), w1 = lds4(sWb + nl * WKP + q * CS + 8 * kq + 4);
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      bw[q][st] = w0[st];
-      bw[q][st + 4] = w1[st];
+      for (int st = 0; st < 4; ++st) {
+        bw[q][st] = w0[st];
+        bw[q][st + 4] = w1[st];
+      }
     }
+    __syncthreads();  // (the staging below overwrites the block matrix)
   }
-  __syncthreads();  // (the staging below overwrites the block matrix)
   if (nrs > 0) {
     stage_small<SP>(g, P.small, n, ys_lo * g.ws, nrs * g.ws, kf, kb, sIn);
   }
@@ -548,6 +584,47 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   const float bias = nl < NCOL ? sb[cb] : 0.f;
   const int nblk = RBb * nbx, ntile = (nblk + 15) / 16;
   const FDiv fnbx = FDiv::make(nbx);
+  if constexpr (M4) {
+    const float b0 = sb[0];
+    const float* wp = sW4 + (lane & 3) * WKP4;  // (lanes 0..3 are the broadcast A block)
+    for (int tile = w; tile < (nblk + 63) / 64; tile += 4) {
+      const int blk = 64 * tile + lane;
+      const int br = fnbx.div(blk), bx = blk - br * nbx, by = bb0 + br;
+      const float* ap[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ys = by - 1 + (q >> 1), xs = bx - 1 + (q & 1);
+        const bool ok = blk < nblk && ys >= ys_lo && ys <= ys_hi && (unsigned)xs < (unsigned)g.ws;
+        ap[q] = ok ? sIn + ((ys - ys_lo) * g.ws + xs) * SP : sZ;
+      }
+      // one accumulator per neighbour (independent chains), summed in neighbour order
+      f32x4 accq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) accq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c4 = 0; c4 < CS / 4; ++c4) {
+        f32x4 a[4], b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[q] = lds4(wp + q * CS + 4 * c4);
+          b[q] = lds4(ap[q] + 4 * c4);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) accq[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(a[q][k], b[q][k], accq[q], 4, 0, 0);
+      }
+      const f32x4 acc = (accq[0] + accq[1]) + (accq[2] + accq[3]);
+      // acc[i]: class i = (cy, cx) of block blk
+      if (blk < nblk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int yb = 2 * by - g.p + (i >> 1), xb = 2 * bx - g.p + (i & 1);
+          if (yb >= yb0 && yb < yb1 && (unsigned)xb < (unsigned)g.wb) sOut[(yb - yb0) * g.wb + xb] = acc[i] + b0;
+        }
+      }
+    }
+  } else
   for (int tile = w; tile < ntile; tile += 4) {
     // A: this lane's block (row nl of the tile), channels 8 kq .. 8 kq + 7 of each neighbour
     const int blk = 16 * tile + nl;
@@ -1210,6 +1287,7 @@ static int edge_scatter_impl(const Geo& g, const cv_operand* in, const float* ws
   size_t lds = ((size_t)a.ipb * g.ws * SP + (size_t)2 * rb * g.wb * cb) * sizeof(float);
   const size_t pre = 4 * ET * sizeof(double) + 16 * (4 * CS + 4) * sizeof(float);  // fold scratch + block matrix
   if (lds < pre) lds = pre;
+  if (cb == 1) lds = ((size_t)m4_off(a.ipb, g.ws, rb, g.wb) + M4_EXTRA) * sizeof(float);  // (>= pre)
   if (lds > 96 * 1024) return -1;
   const void* kern = nullptr;
   const dim3 grid(cdiv(nby, rb), g.n);
@@ -1235,6 +1313,16 @@ static int edge_scatter_impl(const Geo& g, const cv_operand* in, const float* ws
     oa = *o;
   } else {
     CV_EDGE_PICK(edge_scatter_kernel, , false);
+  }
+  {
+    static int m4 = -1;  // CV_EDGE_M4=0: the one-channel image on the 16-column tile (A/B)
+    if (m4 < 0) {
+      const char* e = getenv("CV_EDGE_M4");
+      m4 = e ? atoi(e) != 0 : 1;
+    }
+    if (!m4 && cb == 1)
+      kern = o ? (kk == 3 ? (const void*)edge_scatter_kernel<1, 3, true, false> : (const void*)edge_scatter_kernel<1, 4, true, false>)
+               : (kk == 3 ? (const void*)edge_scatter_kernel<1, 3, false, false> : (const void*)edge_scatter_kernel<1, 4, false, false>);
   }
   if (set_lds(kern, lds)) {
     set_error("edge_scatter: LDS carve-out of %zu bytes refused", lds);

@@ -1293,7 +1293,9 @@ static long wgrad_pm_target(long tiles64 = 0) {
     if (v < 0) v = 0;
   }
   if (v > 0) return v;
-  return tiles64 >= 256 ? tiles64 : 0;
+  // (a target of 256 against >= 256 64-row tiles: the 128-row split is then 1, so wgrad_plan takes 64-row tiles
+  // at split 1 — a target of tiles64 itself would not, wgrad_plan's tile count includes the bias column)
+  return tiles64 >= 256 ? 256 : 0;
 }
 
 static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
@@ -1392,6 +1394,13 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
     }
   }
   a.kchunk = w.kchunk;
+  {
+    static int log = -1;
+    if (log < 0) log = getenv("CV_WGRAD_LOG") ? 1 : 0;
+    if (log)
+      fprintf(stderr, "wgrad M=%d N=%d K=%d pm=%d BM=%d BN=%d split=%d kchunk=%d\n", a.M, a.N, a.K, a.pm, w.BM, w.BN,
+              w.split, w.kchunk);
+  }
   static int atomic_splits = -1;  // A/B knob CV_WGRAD_ATOMIC=1: split-K tiles added with fp32 atomics, no partials
   if (atomic_splits < 0) {
     const char* e = getenv("CV_WGRAD_ATOMIC");

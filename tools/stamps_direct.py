@@ -28,10 +28,23 @@ for pname, P in bench._programs(G):
     for i, c in enumerate(P.calls):
         flat.append((f"{pname}[{i}]", c))
 pos = {lab: k for k, (lab, _) in enumerate(flat)}
+
+
+def _edge_label():  # "@edge": the forward ConvTranspose2d back to the image (<= 4 channels)
+    for lab, c in flat:
+        if lab.startswith("fwd") and c[0].startswith("cv_conv"):
+            g = c[2][0]._obj
+            if g.transposed and g.c_out <= 4:
+                return lab
+    raise SystemExit("no image-side ConvTranspose2d forward call")
+
+
 s_ = _lib.stream_handle()
 q = lambda v: [round(float(v.quantile(x)), 2) for x in (0.0, 0.5, 0.9, 1.0)]
 names = ("constants", "region", "stages", "epilogue", "stats")
 for call in sys.argv[2:]:
+    if call == "@edge":
+        call = _edge_label()
     out = []
     for rep in range(3):
         for lab, (name, fn, cargs, _) in flat[:pos[call]]:

@@ -1,5 +1,5 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for spec in "mnist fwd[8]" "celeba fwd[12]"; do
+for spec in "mnist @edge" "celeba @edge"; do
   set -- $spec
   CVHIP_LIB=scratch/libclearvae_stamps.so timeout -k 10 200 python tools/stamps_direct.py $1 "$2" > gpurun_out/stamps_edge_$1.txt 2>&1 || { tail -20 gpurun_out/stamps_edge_$1.txt; exit 1; }
   python - gpurun_out/stamps_edge_$1.txt <<'PY'
