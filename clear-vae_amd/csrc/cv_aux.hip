@@ -16,6 +16,7 @@
 
 namespace cv {
 thread_local AuxPend g_aux;
+bool ntxent_reg_ok(const NtArgs& a, int nbr);  // (cv_latent.hip)
 
 namespace aux {
 
@@ -24,7 +25,7 @@ struct AuxMap {
   int na, agx;       // aux workgroups and their grid's x extent (row blocks per branch)
 };
 
-template <int OP, int XA, int EPI, int CBT, int FMX, int PHASE, int DM>
+template <int OP, int XA, int EPI, int CBT, int FMX, int PHASE, int DM, bool REG>
 __global__ __launch_bounds__(NT, 2) void direct_aux_kernel(const direct::DArgs PD, const NtArgs PA, const AuxMap m) {
   const int v = blockIdx.x;
   const int k = m.nd < m.na ? m.nd : m.na;
@@ -39,18 +40,22 @@ __global__ __launch_bounds__(NT, 2) void direct_aux_kernel(const direct::DArgs P
   if (role == 0) {
     direct::direct_body<OP, XA, EPI, CBT, FMX>(PD, idx % m.dgx, idx / m.dgx, m.dgx, m.dgy);
   } else if constexpr (PHASE == 0) {
-    ntxent_rows_lds_body<DM>(PA, idx % m.agx, idx / m.agx);
+    if constexpr (REG) ntxent_rows_reg_body<DM, NTR_JM>(PA, idx % m.agx, idx / m.agx);
+    else ntxent_rows_lds_body<DM>(PA, idx % m.agx, idx / m.agx);
   } else {
-    ntxent_grad_lds_body<DM>(PA, idx % m.agx, idx / m.agx);
+    if constexpr (REG) ntxent_grad_reg_body<DM, NTR_JM>(PA, idx % m.agx, idx / m.agx);
+    else ntxent_grad_lds_body<DM>(PA, idx % m.agx, idx / m.agx);
   }
 }
 
 struct Ent {
   int dk[5];  // direct OP, XA, EPI, CBT, FMX
-  int phase, dm;
+  int phase, dm, reg;
   const void* fn;
 };
-#define CV_AUX(a, b, c, d, e, ph, dm) Ent{{a, b, c, d, e}, ph, dm, (const void*)direct_aux_kernel<a, b, c, d, e, ph, dm>}
+#define CV_AUX(a, b, c, d, e, ph, dm)                                                             \
+  Ent{{a, b, c, d, e}, ph, dm, 0, (const void*)direct_aux_kernel<a, b, c, d, e, ph, dm, false>}, \
+      Ent{{a, b, c, d, e}, ph, dm, 1, (const void*)direct_aux_kernel<a, b, c, d, e, ph, dm, true>}
 // MNIST's decoder forward: ConvT1 (SCATTER, untransformed input: the decoder Linear's BN1d + ReLU output) and ConvT2
 // (SCATTER, BN+ReLU input), both with the STAT_FWD epilogue; d <= 8 (the bench's z = 16; a d = 16 gradient phase
 // spilled 12 registers in this grid, so larger latents take the standalone launches)
@@ -79,17 +84,18 @@ int direct_aux_launch(const int* dkey, const direct::DArgs& da, dim3 dgrid, size
   using namespace aux;
   if (!g_aux.set || !enabled()) return -1;
   const NtArgs& pa = g_aux.a;
-  if (pa.with_combine || pa.d > 8 || pa.n > NT_MAXN) return -1;
+  if ((pa.with_combine && g_aux.phase != 0) || pa.d > 8 || pa.n > NT_MAXN) return -1;
   const int dm = 8;
+  const int reg = ntxent_reg_ok(pa, pa.nbr) ? 1 : 0;
   const void* fn = nullptr;
   for (const Ent& e : k_aux) {
-    bool ok = e.phase == g_aux.phase && e.dm == dm;
+    bool ok = e.phase == g_aux.phase && e.dm == dm && e.reg == reg;
     for (int i = 0; i < 5; ++i) ok = ok && e.dk[i] == dkey[i];
     if (ok) fn = e.fn;
   }
   if (!fn) return -1;
   const bool need_lv = !(pa.sim == CV_SIM_COSINE || pa.sim == CV_SIM_L2);
-  size_t alds = ntl_bytes(pa.n, pa.d, need_lv, g_aux.phase == 1);
+  size_t alds = reg ? 0 : ntl_bytes(pa.n, pa.d, need_lv, g_aux.phase == 1);
   if (alds < 16 * sizeof(double)) alds = 16 * sizeof(double);
   const size_t lds = dlds > alds ? dlds : alds;
   if (lds > 144 * 1024) return -1;
@@ -99,7 +105,7 @@ int direct_aux_launch(const int* dkey, const direct::DArgs& da, dim3 dgrid, size
   }
   const long nd = (long)dgrid.x * dgrid.y;
   const int agx = (pa.n + pa.rpb - 1) / pa.rpb;
-  const long na = (long)agx * pa.nbr;
+  const long na = (long)agx * pa.nbr + (pa.with_combine ? 1 : 0);  // (+ the combine block: bx 0, by nbr)
   AuxMap m{(int)nd, (int)dgrid.x, (int)dgrid.y, (int)na, agx};
   direct::DArgs a = da;
   NtArgs b = pa;

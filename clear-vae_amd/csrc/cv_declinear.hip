@@ -422,7 +422,42 @@ struct HeadsArgs {
   float* gw;            // [J][F] +=
   float* gb;            // [J] += (workgroup 0)
   int n, J, F, pix, ch;
+  cv_latent_chain chain;  // chain.dz != nullptr: the decoder chain term is added to dheads while staging it
 };
+
+// stage_pad of dheads [n][J = 4d] with the decoder chain term of cv_latent_combine added (cv_latent_chain): column
+// block b = j / d, latent k = j % d, z index zi = (b / 2) d + k; mu blocks + dz[zi], logvar blocks + dz[zi] (z[zi] -
+// mu[zi]) / 2 (the combine's arithmetic: (g (z - m)) 0.5)
+template <int KR>
+__device__ __forceinline__ void stage_pad_chain(const float* __restrict__ src, int n, int K, const cv_latent_chain& c,
+                                                float* dst) {
+  constexpr int U = 8, P = KR + 4;
+  const int d = c.d, zd = 2 * d;
+  const long total = (long)((n + 15) & ~15) * KR;
+  for (long e0 = threadIdx.x; e0 < total; e0 += (long)NTD * U) {
+    float v[U], g[U], zz[U], m[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long e = e0 + (long)NTD * u;
+      const int row = (int)(e / KR), j = (int)(e % KR);
+      const bool ok = e < total && row < n && j < K;
+      const int r = ok ? row : 0, jj = ok ? j : 0;
+      const int b = jj / d, k = jj - b * d, zi = (b >> 1) * d + k;
+      v[u] = ok ? src[(size_t)row * K + j] : 0.f;
+      g[u] = ok ? c.dz[(size_t)r * zd + zi] : 0.f;
+      zz[u] = (b & 1) ? c.z[(size_t)r * zd + zi] : 0.f;
+      m[u] = (b & 1) ? c.heads[(size_t)r * K + (b - 1) * d + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long e = e0 + (long)NTD * u;
+      if (e >= total) break;
+      const int j = (int)(e % KR);
+      const int b = j < K ? j / d : 0;
+      dst[(e / KR) * P + j] = (b & 1) ? v[u] + g[u] * (zz[u] - m[u]) * 0.5f : v[u] + g[u];
+    }
+  }
+}
 
 template <int JR>
 __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
@@ -444,7 +479,16 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
       const int j = 16 * c + 4 * lq + s;
       b[c][s] = j < J ? A.w[(size_t)j * F + f] : 0.f;
     }
-  stage_pad<JR>(A.dheads, n, J, sd);
+  if (A.chain.dz) {
+    stage_pad_chain<JR>(A.dheads, n, J, A.chain, sd);
+    if (blockIdx.x == 0 && t == 0 && A.chain.rec_in && A.chain.losses) {
+      double r = 0.0;
+      for (int q = 0; q < CV_REC_REPL; ++q) r += A.chain.rec_in[q];
+      A.chain.losses[0] = (float)r;
+    }
+  } else {
+    stage_pad<JR>(A.dheads, n, J, sd);
+  }
   if (t < DF) {  // the layer's forward constants: finalised by its producer, or folded from the replicas
     const int cc = (col0 + t) % C;
     const cv_bn& bn = A.bn;
@@ -821,9 +865,29 @@ extern "C" int cv_heads_backward_supported(int n, int in_features, int in_ch, in
           heads_lds(n, out_features) <= 150 * 1024) ? 1 : 0;
 }
 
+static int heads_backward(const cv_linear* g, const float* dheads, const cv_latent_chain* chain, const float* weight,
+                          const float* y, const cv_bn* bn, float* gin, double* gstat_out, float* gweight, float* gbias,
+                          cv_stream_t stream);
+
 extern "C" int cv_heads_backward(const cv_linear* g, const float* dheads, const float* weight, const float* y,
                                  const cv_bn* bn, float* gin, double* gstat_out, float* gweight, float* gbias,
                                  cv_stream_t stream) {
+  return heads_backward(g, dheads, nullptr, weight, y, bn, gin, gstat_out, gweight, gbias, stream);
+}
+
+extern "C" int cv_heads_backward_chain(const cv_linear* g, const float* dheads, const cv_latent_chain* chain,
+                                       const float* weight, const float* y, const cv_bn* bn, float* gin,
+                                       double* gstat_out, float* gweight, float* gbias, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(chain && chain->heads && chain->z && chain->dz && chain->d > 0, "heads_backward_chain: null chain");
+  CV_REQUIRE(g && g->out_features == 4 * chain->d, "heads_backward_chain: out_features %d != 4 d (d = %d)",
+             g ? g->out_features : -1, chain->d);
+  return heads_backward(g, dheads, chain, weight, y, bn, gin, gstat_out, gweight, gbias, stream);
+}
+
+static int heads_backward(const cv_linear* g, const float* dheads, const cv_latent_chain* chain, const float* weight,
+                          const float* y, const cv_bn* bn, float* gin, double* gstat_out, float* gweight, float* gbias,
+                          cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(g && dheads && weight && y && bn && gin && gweight, "heads_backward: null args");
   const int pix = g->in_pix > 0 ? g->in_pix : 1, ch = pix > 1 ? g->in_ch : g->in_features;
@@ -844,6 +908,8 @@ extern "C" int cv_heads_backward(const cv_linear* g, const float* dheads, const 
   a.F = g->in_features;
   a.pix = pix;
   a.ch = ch;
+  memset(&a.chain, 0, sizeof(a.chain));
+  if (chain) a.chain = *chain;
   const size_t lds = heads_lds(g->n, a.J);
   auto go = [&](auto jr) -> int {
     constexpr int JR = decltype(jr)::value;

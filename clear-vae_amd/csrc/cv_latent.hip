@@ -521,6 +521,35 @@ static int ntxent_launch_fused(const NtArgs& a, int nbr, hipStream_t st) {
   return 0;
 }
 
+template <int DM, int JM>
+__global__ __launch_bounds__(256) void ntxent_rows_reg_kernel(const NtArgs A) {
+  ntxent_rows_reg_body<DM, JM>(A, blockIdx.x, blockIdx.y);
+}
+
+template <int DM, int JM>
+__global__ __launch_bounds__(256) void ntxent_grad_reg_kernel(const NtArgs A) {
+  ntxent_grad_reg_body<DM, JM>(A, blockIdx.x, blockIdx.y);
+}
+
+// the register-resident variants serve this batch (ntr_fits + 16-byte rows); CV_NT_REG=0: never (A/B)
+static int g_nt_reg = -1;  // (cv_debug_nt_reg)
+static int nt_reg_on() {
+  if (g_nt_reg < 0) {
+    const char* e = getenv("CV_NT_REG");
+    g_nt_reg = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_nt_reg;
+}
+bool ntxent_reg_ok(const NtArgs& a, int nbr) {
+  if (!nt_reg_on() || !ntr_fits(a.n, a.d, a.sim)) return false;
+  for (int i = 0; i < nbr; ++i) {
+    const Branch& b = a.br[i];
+    if (b.ld % 4 || (reinterpret_cast<uintptr_t>(b.mu) & 15))
+      return false;
+  }
+  return true;
+}
+
 template <template <int> class K>
 struct DDispatch;
 
@@ -536,6 +565,16 @@ static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st
   arg.rpb = NTL_ROWS;
   arg.nbr = nbr;
   const dim3 grid(cdiv(a.n, arg.rpb), nbr + ((rows && a.with_combine) ? 1 : 0));
+  if (ntxent_reg_ok(a, nbr)) {
+    const void* kr = rows ? (const void*)ntxent_rows_reg_kernel<8, NTR_JM> : (const void*)ntxent_grad_reg_kernel<8, NTR_JM>;
+    void* params[] = {&arg};
+    note_launch(kr);
+    if (hipLaunchKernel(kr, grid, dim3(256), params, 16 * sizeof(double), st) != hipSuccess) {
+      ::cv::set_error("%s: launch failed", rows ? "ntxent_rows" : "ntxent_grad");
+      return 2;
+    }
+    return 0;
+  }
   const void* kern;
   if (a.d <= 8) kern = rows ? (const void*)ntxent_rows_lds_kernel<8> : (const void*)ntxent_grad_lds_kernel<8>;
   else if (a.d <= 16) kern = rows ? (const void*)ntxent_rows_lds_kernel<16> : (const void*)ntxent_grad_lds_kernel<16>;
@@ -744,6 +783,19 @@ extern "C" int cv_ntxent_aux(const cv_ntxent_branch* br, int nbr, const int64_t*
   return 0;
 }
 
+extern "C" int cv_ntxent_aux_combine(const float* heads, const float* z, int n, int d, float beta, float loc,
+                                     float scale, const int64_t* anneal_step, float* dheads, float* losses,
+                                     cv_stream_t stream) {
+  clear_error();
+  (void)stream;
+  CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "ntxent_aux_combine: bad args");
+  CV_REQUIRE(g_aux.set && g_aux.phase == 0, "ntxent_aux_combine: no queued phase-0 request");
+  CV_REQUIRE(g_aux.a.n == n && g_aux.a.d == d, "ntxent_aux_combine: n / d differ from the queued request");
+  g_aux.a.with_combine = 1;
+  g_aux.a.cmb = CombineArgs{heads, z, nullptr, n, d, beta, loc, scale, anneal_step, nullptr, dheads, losses, 0};
+  return 0;
+}
+
 extern "C" int cv_ntxent_aux_flush(cv_stream_t stream) {
   clear_error();
   if (!g_aux.set) return 0;
@@ -772,4 +824,11 @@ extern "C" int cv_latent_step(const float* heads, const float* z, const float* d
   if (ntxent_launch(a, nbr, true, S(stream))) return 2;
   if (ntxent_launch(a, nbr, false, S(stream))) return 2;
   return 0;
+}
+
+// test hook: the register-resident NT-Xent variants on (1) / off (0), -1 = query; returns the previous setting
+extern "C" int cv_debug_nt_reg(int on) {
+  const int prev = cv::nt_reg_on();
+  if (on >= 0) cv::g_nt_reg = on ? 1 : 0;
+  return prev;
 }

@@ -53,6 +53,18 @@ __device__ __forceinline__ void combine_body(const CombineArgs& C, double* scrat
       g[q] = dz ? dz[ec] : 0.f;
       zz[q] = z[ec];
     }
+    // (accumulate: every old d(heads) value of the batch is read before the first store — loads and stores through
+    // one pointer stay in program order, so element-wise read-modify-writes cost one dependent round trip each)
+    float om[U], ol[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = base + q * NTH;
+      const int ec = e < total ? e : 0;
+      const int r = ec / zd, j = ec - r * zd;
+      const int blk = (j < d) ? 0 : 2, k = (j < d) ? j : j - d;
+      om[q] = C.accumulate ? dheads[(size_t)r * 4 * d + blk * d + k] : 0.f;
+      ol[q] = C.accumulate ? dheads[(size_t)r * 4 * d + (blk + 1) * d + k] : 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int e = base + q * NTH;
@@ -64,10 +76,8 @@ __device__ __forceinline__ void combine_body(const CombineArgs& C, double* scrat
       if (j < d) sc += term; else ss += term;
       const float vm = w * m[q] * inv_n + g[q];
       const float vl = w * (-0.5f * inv_n) * (1.0f - el) + g[q] * (zz[q] - m[q]) * 0.5f;
-      float* pm = dheads + (size_t)r * 4 * d + blk * d + k;
-      float* pl = dheads + (size_t)r * 4 * d + (blk + 1) * d + k;
-      *pm = C.accumulate ? *pm + vm : vm;
-      *pl = C.accumulate ? *pl + vl : vl;
+      dheads[(size_t)r * 4 * d + blk * d + k] = C.accumulate ? om[q] + vm : vm;
+      dheads[(size_t)r * 4 * d + (blk + 1) * d + k] = C.accumulate ? ol[q] + vl : vl;
     }
   }
   const double kc = block_sum<NTH>(sc, scratch);
@@ -580,6 +590,173 @@ __device__ __forceinline__ void ntxent_grad_lds_body(const NtArgs& A, const int 
         float* pl = b.dlv + (size_t)i * b.gld + lane;
         *pl = A.accumulate ? *pl + ol : ol;
       }
+    }
+  }
+}
+
+// Register-resident variants for small batches (cosine similarity, n <= 64 * JM, d <= DM, 16-byte rows: MNIST's
+// bs = 512, d = 8).  The LDS kernels above stage the whole branch per workgroup (two dependent HBM/L2 round trips,
+// three barriers and two LDS passes before the first pair), then walk one row per wave: at these sizes the staging
+// is the kernel.  Here every lane requests its JM columns (rows j = lane + 64 m as float4s, the label, and for the
+// gradients the two log-sum-exps) and the wave's own row in ONE batch of loads, normalises in registers and runs
+// the same pair loop.  The arithmetic, and its order, is the LDS kernels' (unit vectors = row / max(|row|, 1e-8),
+// the same dot products, the same per-lane merge order j ascending, the same shuffle tree and 1/n_i placement), so
+// the results are bit-identical to them (tests/test_gpu_ntxent_reg.py).
+constexpr int NTR_JM = 8;
+__host__ __device__ inline bool ntr_fits(int n, int d, int sim) {
+  return sim == CV_SIM_COSINE && n <= 64 * NTR_JM && d <= 8 && d % 4 == 0;
+}
+
+template <int DM>
+__device__ __forceinline__ void ntr_row(const float* p, int d, float* m) {
+#pragma unroll
+  for (int k4 = 0; k4 < DM / 4; ++k4) {
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (4 * k4 < d) v = *reinterpret_cast<const f32x4*>(p + 4 * k4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) m[4 * k4 + c] = v[c];
+  }
+}
+
+// m <- m / max(|m|, 1e-8) (the LDS kernels' staged unit vectors); returns the clamped norm, *raw the norm itself
+template <int DM>
+__device__ __forceinline__ float ntr_unit(float* m, int d, float* raw = nullptr) {
+  const float r = reg_norm<DM>(m, d);
+  const float nr = fmaxf(r, 1e-8f);
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) m[k] = m[k] / nr;
+  if (raw) *raw = r;
+  return nr;
+}
+
+template <int DM, int JM>
+__device__ __forceinline__ void ntxent_rows_reg_body(const NtArgs& A, const int bx, const int by) {
+  extern __shared__ __attribute__((aligned(16))) char ntl_smem[];
+  if (by >= A.nbr) {
+    if (A.with_combine && bx == 0) combine_body<256>(A.cmb, reinterpret_cast<double*>(ntl_smem));
+    return;
+  }
+  const Branch& b = A.br[by];
+  const int n = A.n, d = A.d;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = bx * A.rpb + w;  // (rpb = 4: one row per wave)
+  if (i >= n) return;
+  float mi[DM], mj[JM][DM];
+  long long labj[JM];
+  ntr_row<DM>(b.mu + (size_t)i * b.ld, d, mi);
+  const long long lab = A.label[i];
+#pragma unroll
+  for (int m = 0; m < JM; ++m) {
+    const int j = lane + 64 * m, jc = j < n ? j : i;
+    ntr_row<DM>(b.mu + (size_t)jc * b.ld, d, mj[m]);
+    labj[m] = A.label[jc];
+  }
+  ntr_unit<DM>(mi, d);
+#pragma unroll
+  for (int m = 0; m < JM; ++m) ntr_unit<DM>(mj[m], d);
+  float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
+#pragma unroll
+  for (int m = 0; m < JM; ++m) {
+    const int j = lane + 64 * m;
+    const float s = dot_u<DM>(mi, mj[m], d) / A.tau;
+    if (j < n && j != i) {
+      lse_merge(ma, sa, s, 1.f);
+      const bool pos = b.ps ? (labj[m] != lab) : (labj[m] == lab);
+      if (pos) lse_merge(mp, sp, s, 1.f);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(ma, o, 64), s2 = __shfl_xor(sa, o, 64);
+    const float m3 = __shfl_xor(mp, o, 64), s3 = __shfl_xor(sp, o, 64);
+    lse_merge(ma, sa, m2, s2);
+    lse_merge(mp, sp, m3, s3);
+  }
+  if (lane == 0) {
+    b.lse[i] = (sa > 0.f) ? ma + logf(sa) : -INFINITY;
+    b.lse[n + i] = (sp > 0.f) ? mp + logf(sp) : -INFINITY;
+  }
+}
+
+template <int DM, int JM>
+__device__ __forceinline__ void ntxent_grad_reg_body(const NtArgs& A, const int bx, const int by) {
+  __shared__ float scratch[16];
+  __shared__ double dscratch[16];
+  const Branch& b = A.br[by];
+  const int n = A.n, d = A.d;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = bx * A.rpb + w, ic = i < n ? i : 0;
+  // every load of the pair loop first (their latency overlaps the finite-row count and its barriers)
+  float mi[DM], mj[JM][DM], laj[JM], lpj[JM];
+  long long labj[JM];
+  ntr_row<DM>(b.mu + (size_t)ic * b.ld, d, mi);
+  const long long lab = A.label[ic];
+  const float la_i = b.lse[ic], lp_i = b.lse[n + ic];
+#pragma unroll
+  for (int m = 0; m < JM; ++m) {
+    const int j = lane + 64 * m, jc = j < n ? j : ic;
+    ntr_row<DM>(b.mu + (size_t)jc * b.ld, d, mj[m]);
+    labj[m] = A.label[jc];
+    laj[m] = b.lse[jc];
+    lpj[m] = b.lse[n + jc];
+  }
+  // finite-row count (and, in block 0, the loss)
+  float cnt = 0.f;
+  double lsum = 0.0;
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const float l = b.lse[j] - b.lse[n + j];
+    if (isfinite(l)) {
+      cnt += 1.f;
+      lsum += (double)l;
+    }
+  }
+  const float nf = block_sum<256>(cnt, scratch);
+  if (bx == 0) {
+    const double tot = block_sum<256>(lsum, dscratch);
+    if (threadIdx.x == 0 && b.loss_out) b.loss_out[0] = (nf > 0.f) ? (float)(tot / (double)nf) : NAN;
+  }
+  if (!b.dmu || i >= n) return;
+  const float gup = b.gmul * (b.gscale ? b.gscale[0] : 1.0f);
+  const float c = (nf > 0.f) ? gup / (nf * A.tau) : 0.f;
+  float rawi;
+  const float ni = ntr_unit<DM>(mi, d, &rawi);
+#pragma unroll
+  for (int m = 0; m < JM; ++m) ntr_unit<DM>(mj[m], d);
+  const bool clamped_i = !(rawi > 1e-8f);
+  const bool fin_i = isfinite(la_i - lp_i);
+  float gm[DM];
+#pragma unroll
+  for (int k = 0; k < DM; ++k) gm[k] = 0.f;
+#pragma unroll
+  for (int m = 0; m < JM; ++m) {
+    const int j = lane + 64 * m;
+    const float S = dot_u<DM>(mi, mj[m], d);
+    const float s = S / A.tau;
+    const bool pos = b.ps ? (labj[m] != lab) : (labj[m] == lab);
+    const bool fin_j = isfinite(laj[m] - lpj[m]);
+    float G = 0.f;
+    if (fin_i) G += c * (expf(s - la_i) - (pos ? expf(s - lp_i) : 0.f));
+    if (fin_j) G += c * (expf(s - laj[m]) - (pos ? expf(s - lpj[m]) : 0.f));
+    if (j < n && j != i && G != 0.f) {
+#pragma unroll
+      for (int k = 0; k < DM; ++k)
+        if (k < d) gm[k] += G * (clamped_i ? mj[m][k] : (mj[m][k] - S * mi[k]));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) gm[k] = wave_sum(gm[k]) / ni;
+  float om = 0.f;
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k == lane) om = gm[k];
+  if (lane < d) {
+    float* pm = b.dmu + (size_t)i * b.gld + lane;
+    *pm = A.accumulate ? *pm + om : om;
+    if (b.dlv) {
+      float* pl = b.dlv + (size_t)i * b.gld + lane;
+      *pl = A.accumulate ? *pl + 0.f : 0.f;  // (the LDS kernel adds its zero logvar gradient)
     }
   }
 }

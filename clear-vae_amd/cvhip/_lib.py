@@ -114,6 +114,11 @@ class cv_tc_grad(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("w1", "b1", "w2", "b2")]
 
 
+class cv_latent_chain(ctypes.Structure):
+    _fields_ = [("heads", c_void_p), ("z", c_void_p), ("dz", c_void_p), ("d", c_int), ("rec_in", c_void_p),
+                ("losses", c_void_p)]
+
+
 class cv_ntxent_branch(ctypes.Structure):
     _fields_ = [
         ("mu", c_void_p),
@@ -231,6 +236,11 @@ _SIGS = {
         c_int,
         [_P(cv_linear), c_void_p, c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "cv_heads_backward_chain": (
+        c_int,
+        [_P(cv_linear), c_void_p, _P(cv_latent_chain), c_void_p, c_void_p, _P(cv_bn), c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p],
+    ),
     "cv_bn_apply": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cv_bn_update_running": (c_int, [_P(cv_bn), c_int, c_float, _P(c_void_p), c_void_p]),
     "cv_bn_batch_stats": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_void_p]),
@@ -271,6 +281,10 @@ _SIGS = {
         [_P(cv_ntxent_branch), c_int, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
     ),
     "cv_ntxent_aux_flush": (c_int, [c_void_p]),
+    "cv_ntxent_aux_combine": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "cv_latent_combine_acc": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
@@ -354,6 +368,7 @@ _SIGS = {
     "cv_debug_pm": (c_int, [c_int]),
     "cv_debug_aux": (c_int, [c_int]),
     "cv_debug_aux_count": (c_int, [c_int]),
+    "cv_debug_nt_reg": (c_int, [c_int]),
     "cv_debug_pm_count": (c_int, [c_int]),
     "cv_debug_dual_count": (c_int, [c_int]),
     "cv_debug_kernel_log": (c_int, [c_int]),

@@ -42,7 +42,8 @@ import torch.distributed as dist
 
 from . import _lib, rng
 from . import dist as cvdist
-from ._lib import GROUP, MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_mlp, cv_mlp_grad, cv_ntxent_branch, cv_tc_disc, cv_tc_grad
+from ._lib import (GROUP, MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_latent_chain, cv_mlp, cv_mlp_grad, cv_ntxent_branch,
+                   cv_tc_disc, cv_tc_grad)
 from .autograd import est_params, mlp_struct
 from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
 
@@ -78,6 +79,17 @@ LATENT_SIDE = os.environ.get("CVHIP_LATENT_SIDE", "0") == "1"
 # decoder backward (cv_latent_combine_acc).  One stream, no graph edges; d(heads) is bit-identical (the same two adds
 # per element, in the other order).
 LATENT_AUX = os.environ.get("CVHIP_LATENT_AUX", "1") == "1"
+
+# CVHIP_LATENT_CHAIN=1 (A/B knob, off; with LATENT_AUX): the latent combine split at its dependency.  Its KL part (losses
+# 1, 2, 7 and the KL gradient, written into the zeroed d(heads)) needs only the heads, so it rides as one more
+# workgroup of the rows phase's grid (cv_ntxent_aux_combine); its decoder-chain part needs dz, which the decoder
+# backward produces, and is added by the fused heads backward as it stages d(heads) (cv_heads_backward_chain, which
+# also writes losses[0]).  The step loses the one-workgroup combine launch between the decoder and the encoder
+# backward.  d(heads) in memory then holds the KL + contrastive (+ MI) terms only; the sums differ from the
+# one-launch combine's by the order of two fp32 adds per element.  Opt-in (measured slower, round 5: MNIST 0.5025
+# -> 0.5145 ms — the chain term's three extra operands cost the heads backward's staging 13.0 -> 22.3 us, more than
+# the combine launch it replaces, and the KL workgroup lengthened the rows-phase grid by 12 us).
+LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 
 
 def disc_params(disc):
@@ -361,6 +373,12 @@ class ClearStep:
         tau_c = ctypes.c_float(float(hp["temperature"])) if br_arr is not None else None
         aux_args = ([(br_arr, len(branches), lab, n, d, self.sim, tau_c, ph, 1) for ph in (0, 1)]
                     if aux_nt else None)
+        chain_nt = aux_nt and LATENT_CHAIN and ws.fused_heads()
+        hpf = lambda k, dflt: ctypes.c_float(float(hp.get(k, dflt)))
+        aux_comb = ((ws.heads, ws.z, n, d, hpf("beta", 0), hpf("loc", 0), hpf("scale", 1), self.anneal, ws.dheads,
+                     ws.losses) if chain_nt else None)
+        chain = (cv_latent_chain(ws.heads.data_ptr(), ws.z.data_ptr(), ws.dz.data_ptr(), d, ws.rec.data_ptr(),
+                                 ws.losses.data_ptr()) if chain_nt else None)
 
         def make_fwd(inject: bool):
             f = Program()
@@ -386,7 +404,8 @@ class ClearStep:
                 ws.decoder_program(f, ws.z, True, "loss", X, rec_scale=gscale_rec)
                 f.keep += [gwork, gscale_rec]
             else:
-                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp, aux=aux_args)
+                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp, aux=aux_args,
+                                   aux_combine=aux_comb)
                 if aux_nt:
                     f.keep.append(br_arr)
             # (the running statistics are folded at the end of the backward by cv_step_reduce)
@@ -412,6 +431,8 @@ class ClearStep:
                     ctypes.c_float(float(hp.get("scale", 1))), self.anneal, ws.rec, ws.dheads, ws.losses)
             lat_inj = lat
             lat.keep.append(gwork)
+        elif chain_nt:  # (the combine's two parts ride in the rows-phase grid and in the heads backward)
+            lat_inj = Program()
         elif side_nt or aux_nt:
             # (side stream: join it first) the KL + decoder-chain seed added onto the NT-Xent gradients
             if side_nt:
@@ -455,7 +476,8 @@ class ClearStep:
             k = self._enc_split()
             nl = len(sp.enc)
             enc_defer2 = DeferGroup()
-            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, layers=range(nl - 1, k - 1, -1))
+            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, layers=range(nl - 1, k - 1, -1),
+                                        chain=chain)
             ws.step_reduce_program(enc, enc_defer, pg, ws.bn_enc[k:], running=False)
             enc2 = Program()
             ws.encoder_backward_program(enc2, pg, ws.dheads, x=X, defer=enc_defer2, heads=False,
@@ -463,7 +485,7 @@ class ClearStep:
             ws.step_reduce_program(enc2, enc_defer2, pg, ws.bn_enc[:k], running=False)
             ws.running_program(enc2, "all")
         else:
-            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer)
+            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, chain=chain)
         upd = Program()
         if dp:
             upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,

@@ -783,10 +783,11 @@ class Workspace:
         return self.FUSED_HEADS and bool(_lib.lib().cv_heads_backward_supported(self.n, sp.F, C, 4 * sp.d))
 
     def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None,
-                        aux=None):
+                        aux=None, aux_combine=None):
         """reparam = (eps, seed, offset): z is drawn from self.heads first (cv_reparam_forward, or inside the
         fused decoder-input launch); None: z is given.  aux: cv_ntxent_aux argument tuples, the i-th queued before
-        the i-th decoder conv (its phase rides in that launch where served) and flushed right after it."""
+        the i-th decoder conv (its phase rides in that launch where served) and flushed right after it;
+        aux_combine: cv_ntxent_aux_combine arguments attached to the first (the KL part of the latent combine)."""
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
@@ -821,6 +822,8 @@ class Workspace:
                 return
             if aux is not None and li < len(aux):
                 P.add("cv_ntxent_aux", *aux[li])
+                if li == 0 and aux_combine is not None:
+                    P.add("cv_ntxent_aux_combine", *aux_combine)
             P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, self.y_dec[li], ep)
             if aux is not None and li < len(aux):
                 P.add("cv_ntxent_aux_flush")
@@ -864,13 +867,21 @@ class Workspace:
         P.add("cv_linear_backward_data", lin, gout, sp.dec_lin.weight, dz_out, 1, ep_none())
 
     def encoder_backward_program(self, P: Program, param_grad, dheads, x=None, dx=None, defer=None, heads=True,
-                                 layers=None):
+                                 layers=None, chain=None):
         """From d(heads) [n, 4d] to the encoder / heads parameter gradients (and dx if asked).  A data-parallel
         step splits it in two programs at a layer boundary (heads=False and `layers`, the conv layers in
-        backward order, for the second) so the first part's gradient bucket is reduced during the second."""
+        backward order, for the second) so the first part's gradient bucket is reduced during the second.
+        chain: a cv_latent_chain whose decoder-chain term the fused heads backward adds to dheads as it reads it
+        (cv_heads_backward_chain; requires fused_heads())."""
         sp, n = self.spec, self.n
         C, Hh, Wh = sp.feat
-        if heads and self.fused_heads():
+        if heads and chain is not None:
+            assert self.fused_heads()
+            lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, LIN_MMA)
+            P.add("cv_heads_backward_chain", lin, dheads, chain, sp.heads[0].weight, self.y_enc[-1],
+                  self.bn_enc[-1].cv(True), self.g_enc[-1], self.bn_enc[-1].gstat, param_grad(sp.heads[0].weight),
+                  param_grad(sp.heads[0].bias))
+        elif heads and self.fused_heads():
             lin = cv_linear(n, sp.F, 4 * sp.d, Hh * Wh, C, 1, 0, LIN_MMA)
             P.add("cv_heads_backward", lin, dheads, sp.heads[0].weight, self.y_enc[-1], self.bn_enc[-1].cv(True),
                   self.g_enc[-1], self.bn_enc[-1].gstat, param_grad(sp.heads[0].weight), param_grad(sp.heads[0].bias))

@@ -268,6 +268,23 @@ int cv_heads_forward(const cv_linear* g, const float* y, const cv_bn* bn, const 
 int cv_heads_backward_supported(int n, int in_features, int in_ch, int out_features);
 int cv_heads_backward(const cv_linear* g, const float* dheads, const float* weight, const float* y, const cv_bn* bn,
                       float* gin, double* gstat_out, float* gweight, float* gbias, cv_stream_t stream);
+/* The decoder gradient chained through the reparameterisation z = mu + eps * exp(logvar / 2) (vae.py:56-60),
+ * applied by cv_heads_backward_chain while it stages dheads: column block b of a row (mu_c, lv_c, mu_s, lv_s) gets
+ * + dz[z index] (mu blocks) or + dz * (z - mu) / 2 (logvar blocks), z index = (b / 2) * d + k — the chain term of
+ * cv_latent_combine, so that the KL part of the combine can run earlier in the step (cv_ntxent_aux_combine) and
+ * the decoder's dz is consumed where dheads is.  dheads itself is not rewritten.  rec_in / losses (optional):
+ * losses[0] = the sum of the CV_REC_REPL replicas of rec_in. */
+typedef struct cv_latent_chain {
+  const float* heads;  /* [n][4d] */
+  const float* z;      /* [n][2d] */
+  const float* dz;     /* [n][2d] */
+  int d;
+  const double* rec_in;
+  float* losses;
+} cv_latent_chain;
+int cv_heads_backward_chain(const cv_linear* g, const float* dheads, const cv_latent_chain* chain, const float* weight,
+                            const float* y, const cv_bn* bn, float* gin, double* gstat_out, float* gweight,
+                            float* gbias, cv_stream_t stream);
 
 /* out = max(BN(x), 0) elementwise for a BatchNorm1d over `features` PyTorch-order features whose
  * tensor is stored in the Unflatten/NHWC order (pix, ch) (vae.py:34-36); rows = batch. */
@@ -376,6 +393,12 @@ int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, 
 int cv_ntxent_aux(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim, float temperature,
                   int phase, int accumulate, cv_stream_t stream);
 int cv_ntxent_aux_flush(cv_stream_t stream);
+/* Attach the KL part of the latent combine (cv_latent_combine with dz = NULL and rec_in = NULL: losses[1], [2], [7]
+ * and dheads = the KL gradient, overwritten — dheads must not hold anything yet) to the queued phase-0 request, as
+ * one more workgroup of the same grid (or of the flush launch).  The decoder chain term follows in
+ * cv_heads_backward_chain.  Requires a queued phase 0 (else an error). */
+int cv_ntxent_aux_combine(const float* heads, const float* z, int n, int d, float beta, float loc, float scale,
+                          const int64_t* anneal_step, float* dheads, float* losses, cv_stream_t stream);
 
 /* The fused step's latent terms in two launches (trainer.py:452-480): cv_latent_combine (KL with the
  * annealer weight, the decoder gradient chained through z) and cv_ntxent phase 2 with accumulate = 1
@@ -573,6 +596,9 @@ int cv_debug_pm_count(int reset);
 int cv_debug_aux(int on);
 /* test hook: direct + NT-Xent grids issued since the last reset */
 int cv_debug_aux_count(int reset);
+/* Test hook: the register-resident NT-Xent variants (cosine, n <= 512, d <= 8; cv_ntxent.hpp) on (1) / off (0:
+ * the LDS-staged kernels), -1 queries; returns the previous setting.  Diagnostics only. */
+int cv_debug_nt_reg(int on);
 /* test hook: dual grids issued since the last reset */
 int cv_debug_dual_count(int reset);
 /* measurement hook: 1 starts recording (on this thread) the kernels the conv / linear calls launch, clearing the

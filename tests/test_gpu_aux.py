@@ -10,7 +10,9 @@ with the previous schedule (cv_latent_step after the decoder backward):
     adds per element in the other order; the remaining run-to-run spread is the fp32-atomic dz partials);
   * both match the fp64 oracle at the parity bar (1e-4 on the losses).
 Also with the merge switched off in the library (cv_debug_aux(0)): the queued phases launch on their own at the
-flush points, same results."""
+flush points, same results.  Both with the combine split (LATENT_CHAIN, default: its KL part rides in the rows-phase
+grid, the decoder-chain part in the heads backward — d(heads) in memory then lacks the chain term, which the test
+adds from z / dz / heads) and with the one-launch combine after the decoder backward."""
 
 import numpy as np
 import pytest
@@ -21,15 +23,16 @@ pytestmark = pytest.mark.gpu
 N = 512
 
 
-def _run(aux_engine, aux_lib):
+def _run(aux_engine, aux_lib, chain=True):
     from oracle import cpu_ref as R
     from cvhip import _lib, engine, rng
     from cvhip.engine import ClearStep
     from test_gpu_parity import _fused_trainer
 
     L = _lib.lib()
-    prev_e, prev_l = engine.LATENT_AUX, L.cv_debug_aux(1 if aux_lib else 0)
+    prev_e, prev_l, prev_c = engine.LATENT_AUX, L.cv_debug_aux(1 if aux_lib else 0), engine.LATENT_CHAIN
     engine.LATENT_AUX = aux_engine
+    engine.LATENT_CHAIN = chain
     try:
         sd = R.det_state("VAE", 16, 1)
         x, label, ec, es, _ = R.det_inputs(N, 1, 28, 16, 10)
@@ -43,7 +46,8 @@ def _run(aux_engine, aux_lib):
 
         def grab():
             ws = eng.last_workspace(N)
-            held.update(heads=ws.heads.clone().cpu(), dheads=ws.dheads.clone().cpu(),
+            held.update(heads=ws.heads.clone().cpu(), dheads=ws.dheads.clone().cpu(), z=ws.z.clone().cpu(),
+                        dz=ws.dz.clone().cpu(),
                         grads={k: p.grad.detach().clone().cpu() for k, p in tr.model.named_parameters()})
 
         losses = eng.step(torch.tensor(x, dtype=torch.float32, device="cuda"), torch.tensor(label, device="cuda"),
@@ -52,6 +56,7 @@ def _run(aux_engine, aux_lib):
         merged = L.cv_debug_aux_count(1)
     finally:
         engine.LATENT_AUX = prev_e
+        engine.LATENT_CHAIN = prev_c
         L.cv_debug_aux(prev_l)
     return dict(losses=losses, merged=merged, **held), (x, label, ec, es, hp, sd)
 
@@ -61,14 +66,18 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
+@pytest.mark.parametrize("chain", [True, False], ids=["chain", "combine-launch"])
 @pytest.mark.parametrize("aux_lib", [True, False], ids=["merged", "standalone-at-flush"])
-def test_aux_schedule_matches_latent_step(aux_lib):
+def test_aux_schedule_matches_latent_step(aux_lib, chain):
     from oracle import cpu_ref as R
+    from test_gpu_declinear import _chain_torch
 
-    new, inp = _run(True, aux_lib)
+    new, inp = _run(True, aux_lib, chain)
     old, _ = _run(False, True)
     assert new["merged"] == (2 if aux_lib else 0), new["merged"]
     assert old["merged"] == 0
+    if chain:  # (d(heads) in memory holds the KL + contrastive terms; the heads backward adds the chain term)
+        new["dheads"] = _chain_torch(new["dheads"], new["heads"], new["z"], new["dz"], 16 // 2)
     for k in ("heads", "dheads"):
         assert _rel(new[k], old[k]) < 1e-6, (k, _rel(new[k], old[k]))
     assert _rel(new["losses"][:5], old["losses"][:5]) < 1e-6, (new["losses"][:5], old["losses"][:5])

@@ -218,6 +218,77 @@ def test_heads_backward(n, C, pix, J, finalise):
         assert float(cbwd.abs().max()) == 0.0
 
 
+def _chain_torch(dheads, heads, z, dz, d):
+    """dheads + the decoder chain term of cv_latent_combine (vae.py:56-60 through z = mu + eps exp(lv / 2)), in
+    the kernel's fp32 operation order."""
+    full = dheads.clone()
+    for b in range(4):
+        zi = slice((b >> 1) * d, (b >> 1) * d + d)
+        cols = slice(b * d, (b + 1) * d)
+        if b % 2 == 0:
+            full[:, cols] = dheads[:, cols] + dz[:, zi]
+        else:
+            full[:, cols] = dheads[:, cols] + dz[:, zi] * (z[:, zi] - heads[:, (b - 1) * d:b * d]) * 0.5
+    return full
+
+
+@pytest.mark.parametrize("n,C,pix,J", HEADS)
+def test_heads_backward_chain(n, C, pix, J):
+    """cv_heads_backward_chain (the decoder chain term added while dheads is staged, engine LATENT_CHAIN) is
+    cv_heads_backward of dheads + that term: bit-identical outputs (the BN backward sums, fp64 atomics of several
+    workgroups, to 1e-12), dheads left as it was, losses[0] = the rec replicas' sum."""
+    from cvhip import _lib
+
+    dev = torch.device("cuda")
+    F, d = C * pix, J // 4
+    g = np.random.default_rng(7 * n + J)
+    t = lambda *sh: torch.tensor(g.standard_normal(sh), dtype=torch.float32, device=dev)
+    dheads, heads, z, dz = t(n, J), t(n, J), t(n, 2 * d), t(n, 2 * d)
+    W = torch.tensor(g.uniform(-0.05, 0.05, (J, F)), dtype=torch.float32, device=dev)
+    y = t(n, F) + 0.3
+    gamma = torch.tensor(g.uniform(0.5, 1.5, C), dtype=torch.float32, device=dev)
+    beta = torch.tensor(g.uniform(-0.3, 0.3, C), dtype=torch.float32, device=dev)
+    R = _lib.stat_repl(C)
+    yc = y.double().view(n * pix, C)
+    stat = torch.zeros(R, 2, C, dtype=torch.float64, device=dev)
+    stat[0, 0] = yc.sum(0)
+    stat[0, 1] = (yc * yc).sum(0)
+    rec = torch.tensor(g.uniform(0, 1, _lib.REC_REPL), dtype=torch.float64, device=dev)
+    losses = torch.zeros(24, device=dev)
+    lin = _lib.cv_linear(n, F, J, pix, C, 1, 0, 0)
+    outs = []
+    for chained in (True, False):
+        gstat = torch.zeros(R, 2, C, dtype=torch.float64, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        bn = _lib.cv_bn(gamma.data_ptr(), beta.data_ptr(), stat.data_ptr(), gstat.data_ptr(), rm.data_ptr(),
+                        rv.data_ptr(), C, n * pix, 1, 1e-5, None, None, None)
+        gin = torch.empty(n, F, device=dev)
+        gw = torch.zeros(J, F, device=dev)
+        gb = torch.zeros(J, device=dev)
+        before = dheads.clone()
+        if chained:
+            ch = _lib.cv_latent_chain(heads.data_ptr(), z.data_ptr(), dz.data_ptr(), d, rec.data_ptr(),
+                                      losses.data_ptr())
+            _lib.call("cv_heads_backward_chain", ctypes.byref(lin), dheads.data_ptr(), ctypes.byref(ch), W.data_ptr(),
+                      y.data_ptr(), ctypes.byref(bn), gin.data_ptr(), gstat.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                      _lib.stream_handle())
+        else:
+            full = _chain_torch(dheads, heads, z, dz, d)
+            _lib.call("cv_heads_backward", ctypes.byref(lin), full.data_ptr(), W.data_ptr(), y.data_ptr(),
+                      ctypes.byref(bn), gin.data_ptr(), gstat.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                      _lib.stream_handle())
+        torch.cuda.synchronize()
+        assert torch.equal(dheads, before)
+        outs.append((gin.cpu(), gw.cpu(), gb.cpu(), gstat.cpu()))
+    for a, b, name in zip(outs[0][:3], outs[1][:3], ("gin", "gw", "gb")):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), (name, (a - b).abs().max())
+    assert _rel(outs[0][3], outs[1][3]) < 1e-12
+    r = 0.0
+    for v in rec.cpu().tolist():  # (the kernel's order)
+        r += v
+    assert float(losses[0]) == float(np.float32(r))
+
+
 HEADS_FWD = [  # n, C, (Hh, Wh), d
     (512, 128, (4, 4), 8),
     (256, 512, (2, 2), 32),
