@@ -121,6 +121,19 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
         (void)hipGetLastError();
         ok = false;
       }
+      {
+        static int log = -1;
+        if (log < 0) log = getenv("CV_DUAL_LOG") ? 1 : 0;
+        if (log) {
+          int occ = -1, occd = -1, occg = -1;
+          (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NT, lds);
+          (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occd, d.kern, NT, d.lds);
+          (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occg, g.kern, NT, g.lds);
+          (void)hipGetLastError();
+          fprintf(stderr, "dual nd=%ld ng=%ld (grid %ux%ux%u) lds d=%zu g=%zu occ dual=%d direct=%d gemm=%d\n", nd, ng,
+                  g.grid.x, g.grid.y, g.grid.z, d.lds, g.lds, occ, occd, occg);
+        }
+      }
       if (ok) {
         DualMap m{(int)nd, (int)d.grid.x, (int)d.grid.y, (int)ng, (int)g.grid.x, (int)g.grid.y, (int)g.grid.z};
         void* params[] = {&d.a, &g.a, &m};
@@ -155,6 +168,33 @@ static thread_local fast::GemmCap t_gcap;
 int dual_wgrad_bm_cap() {  // (only when the captured direct launch belongs to a served pair)
   if (!direct::g_direct_cap || !t_dcap.got || !dual::enabled()) return 0;
   return ((long)t_dcap.grid.x * t_dcap.grid.y <= dual::kMaxDirect && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
+}
+
+// Workgroup slots the weight-gradient role of a served dual grid has in the grid's first resident round (0: no
+// target): CUs x the dual kernel's workgroups per CU (LDS-bound: the larger of the direct role's carve-out and
+// ~40 KB for the 64x64 WGRAD tile's) minus the direct role's workgroups.  CV_DUAL_WTARGET=1 (A/B, default off):
+// the WGRAD split is cut so the whole grid is resident at once.
+long dual_wgrad_slots() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CV_DUAL_WTARGET");
+    on = e ? atoi(e) : 0;
+  }
+  if (!on || !dual_wgrad_bm_cap()) return 0;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = -1;
+    (void)hipGetLastError();
+  }
+  if (cus <= 0) return 0;
+  const size_t lds = t_dcap.lds > 40 * 1024 ? t_dcap.lds : 40 * 1024;
+  long per = (long)(160 * 1024 / lds);
+  if (per > 4) per = 4;  // (the roles' registers: 4 workgroups of 4 waves)
+  const long nd = (long)t_dcap.grid.x * t_dcap.grid.y;
+  const long free = per * cus - nd;
+  return free >= 128 ? free : 0;
 }
 
 void dual_begin() {

@@ -1285,6 +1285,8 @@ static WPlan wgrad_plan(int M, int N, long K, int split_k, int cap_ovr = -1, lon
 // split-K partials for cv_step_reduce (C3's conv5 pair 189.9 -> 160.3 us in-step); below that (conv4 / convT2: 128
 // tiles) the plain target's split stays (256 there measured the pair 168 -> 187 us).  CV_PM_WTARGET: a fixed target
 // (A/B).
+long dual_wgrad_slots();  // (cv_dual.hip)
+
 static long wgrad_pm_target(long tiles64 = 0) {
   static long v = -1;
   if (v < 0) {
@@ -1378,6 +1380,11 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   if (a.pm && split_k <= 0) {
     const long tg = wgrad_pm_target((long)cdiv(a.M, 64) * cdiv(Ntot, w.BN));
     if (tg > 0) w = wgrad_plan(a.M, a.N, a.K, split_k, -1, tg);
+  }
+  if (split_k <= 0) {  // inside a served dual grid: at most the slots its first resident round leaves (A/B knob)
+    const long free = dual_wgrad_slots();
+    const long tiles = (long)cdiv(a.M, w.BM) * cdiv(Ntot, w.BN);
+    if (free > 0 && tiles * w.split > free && free >= tiles) w = wgrad_plan(a.M, a.N, a.K, split_k, -1, (free / tiles) * tiles);
   }
   if (split_k <= 0 && w.split > 1) {
     // one round of resident workgroups: a second, partial round costs a whole extra workgroup time
