@@ -15,7 +15,7 @@ bench)
   tail -c 600 $O/bench.json; echo
   ;;
 trace)
-  for cfg in mnist celeba-mim celeba pacs camelyon-bf16; do
+  for cfg in mnist celeba-mim celeba pacs camelyon-bf16 camelyon-fp32; do
     steps=50; [ $cfg = celeba-mim ] && steps=30
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$cfg -o run -- \
       python3 bench.py --config $cfg --steps $steps --warmup 10 --no-cpu-baseline --no-c3 --no-kernel-pass \
@@ -29,7 +29,8 @@ pmc)
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 keys = [("mnist", d), ("celeba-mim", d.get("c3") or {}), ("celeba", d.get("celeba") or {}),
-        ("pacs", d.get("pacs") or {}), ("camelyon-bf16", d.get("camelyon_bf16") or {})]
+        ("pacs", d.get("pacs") or {}), ("camelyon-bf16", d.get("camelyon_bf16") or {}),
+        ("camelyon-fp32", d.get("camelyon_fp32") or {})]
 for cfg, e in keys:
     r = e.get("roofline") or {}
     if r.get("kernel"):
