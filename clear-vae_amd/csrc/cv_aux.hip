@@ -107,6 +107,17 @@ int direct_aux_launch(const int* dkey, const direct::DArgs& da, dim3 dgrid, size
   const int agx = (pa.n + pa.rpb - 1) / pa.rpb;
   const long na = (long)agx * pa.nbr + (pa.with_combine ? 1 : 0);  // (+ the combine block: bx 0, by nbr)
   AuxMap m{(int)nd, (int)dgrid.x, (int)dgrid.y, (int)na, agx};
+  {
+    static int log = -1;
+    if (log < 0) log = getenv("CV_AUX_LOG") ? 1 : 0;
+    if (log) {
+      int occ = -1;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NT, lds);
+      (void)hipGetLastError();
+      fprintf(stderr, "aux phase=%d reg=%d nd=%ld na=%ld dlds=%zu alds=%zu occ=%d\n", g_aux.phase, reg, nd, na, dlds,
+              alds, occ);
+    }
+  }
   direct::DArgs a = da;
   NtArgs b = pa;
   void* params[] = {&a, &b, &m};

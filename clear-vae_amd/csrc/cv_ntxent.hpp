@@ -621,6 +621,10 @@ __device__ __forceinline__ void ntr_row(const float* p, int d, float* m) {
 // m <- m / max(|m|, 1e-8) (the LDS kernels' staged unit vectors); returns the clamped norm, *raw the norm itself
 template <int DM>
 __device__ __forceinline__ float ntr_unit(float* m, int d, float* raw = nullptr) {
+#if defined(CV_NT_ABLATE) && CV_NT_ABLATE == 1
+  if (raw) *raw = 1.f;  // diagnostic build: no normalisation (results invalid: a timing probe only)
+  return 1.f;
+#endif
   const float r = reg_norm<DM>(m, d);
   const float nr = fmaxf(r, 1e-8f);
 #pragma unroll
