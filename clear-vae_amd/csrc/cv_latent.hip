@@ -540,6 +540,19 @@ static int nt_reg_on() {
   }
   return g_nt_reg;
 }
+// rows per workgroup of the register variants: the workgroup's column loads serve all of them (a multiple of 4: one
+// row per wave per pass).  CV_NT_ROWS overrides (A/B; MNIST step with the phases in the decoder grids: 4 / 8 rows
+// 0.4992 / 0.4991 ms, 16 rows 0.5058, 32 rows 0.5369 — a longer aux workgroup becomes its grid's tail)
+int ntr_rows() {
+  static int r = -1;
+  if (r < 0) {
+    const char* e = getenv("CV_NT_ROWS");
+    r = e ? atoi(e) : 4;
+    if (r < 4 || r % 4) r = 4;
+  }
+  return r;
+}
+
 bool ntxent_reg_ok(const NtArgs& a, int nbr) {
   if (!nt_reg_on() || !ntr_fits(a.n, a.d, a.sim)) return false;
   for (int i = 0; i < nbr; ++i) {
@@ -566,6 +579,8 @@ static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st
   arg.nbr = nbr;
   const dim3 grid(cdiv(a.n, arg.rpb), nbr + ((rows && a.with_combine) ? 1 : 0));
   if (ntxent_reg_ok(a, nbr)) {
+    arg.rpb = ntr_rows();
+    const dim3 grid(cdiv(a.n, arg.rpb), nbr + ((rows && a.with_combine) ? 1 : 0));
     const void* kr = rows ? (const void*)ntxent_rows_reg_kernel<8, NTR_JM> : (const void*)ntxent_grad_reg_kernel<8, NTR_JM>;
     void* params[] = {&arg};
     note_launch(kr);
@@ -771,8 +786,8 @@ extern "C" int cv_ntxent_aux(const cv_ntxent_branch* br, int nbr, const int64_t*
   CV_REQUIRE(phase == 0 || phase == 1, "ntxent_aux: phase %d (0 rows, 1 gradients)", phase);
   NtArgs a;
   if (ntxent_args(br, nbr, label, n, d, sim, temperature, accumulate, a)) return 1;
-  a.rpb = NTL_ROWS;
   a.nbr = nbr;
+  a.rpb = ntxent_reg_ok(a, nbr) ? ntr_rows() : NTL_ROWS;
   if (g_aux.set) {  // a phase no launch took (its flush was skipped): it runs now, in queue order
     g_aux.set = 0;
     if (ntxent_launch(g_aux.a, g_aux.a.nbr, g_aux.phase == 0, S(stream))) return 2;

@@ -603,6 +603,7 @@ __device__ __forceinline__ void ntxent_grad_lds_body(const NtArgs& A, const int 
 // the same dot products, the same per-lane merge order j ascending, the same shuffle tree and 1/n_i placement), so
 // the results are bit-identical to them (tests/test_gpu_ntxent_reg.py).
 constexpr int NTR_JM = 8;
+int ntr_rows();  // rows per 256-thread workgroup of the register variants (cv_latent.hip; CV_NT_ROWS A/B)
 __host__ __device__ inline bool ntr_fits(int n, int d, int sim) {
   return sim == CV_SIM_COSINE && n <= 64 * NTR_JM && d <= 8 && d % 4 == 0;
 }
@@ -644,42 +645,47 @@ __device__ __forceinline__ void ntxent_rows_reg_body(const NtArgs& A, const int 
   const Branch& b = A.br[by];
   const int n = A.n, d = A.d;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int i = bx * A.rpb + w;  // (rpb = 4: one row per wave)
-  if (i >= n) return;
-  float mi[DM], mj[JM][DM];
+  const int i0 = bx * A.rpb + w;  // (the wave's rows: i0, i0 + 4, ... below (bx + 1) rpb)
+  if (i0 >= n) return;
+  // the columns (rows j = lane + 64 m) are the same for every row of the workgroup: loaded and normalised once
+  float mj[JM][DM];
   long long labj[JM];
-  ntr_row<DM>(b.mu + (size_t)i * b.ld, d, mi);
-  const long long lab = A.label[i];
 #pragma unroll
   for (int m = 0; m < JM; ++m) {
-    const int j = lane + 64 * m, jc = j < n ? j : i;
+    const int j = lane + 64 * m, jc = j < n ? j : 0;
     ntr_row<DM>(b.mu + (size_t)jc * b.ld, d, mj[m]);
     labj[m] = A.label[jc];
   }
-  ntr_unit<DM>(mi, d);
 #pragma unroll
   for (int m = 0; m < JM; ++m) ntr_unit<DM>(mj[m], d);
-  float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
+  const int iend = min(n, (bx + 1) * A.rpb);
+  for (int i = i0; i < iend; i += 4) {
+    float mi[DM];
+    ntr_row<DM>(b.mu + (size_t)i * b.ld, d, mi);
+    const long long lab = A.label[i];
+    ntr_unit<DM>(mi, d);
+    float ma = -INFINITY, sa = 0.f, mp = -INFINITY, sp = 0.f;
 #pragma unroll
-  for (int m = 0; m < JM; ++m) {
-    const int j = lane + 64 * m;
-    const float s = dot_u<DM>(mi, mj[m], d) / A.tau;
-    if (j < n && j != i) {
-      lse_merge(ma, sa, s, 1.f);
-      const bool pos = b.ps ? (labj[m] != lab) : (labj[m] == lab);
-      if (pos) lse_merge(mp, sp, s, 1.f);
+    for (int m = 0; m < JM; ++m) {
+      const int j = lane + 64 * m;
+      const float s = dot_u<DM>(mi, mj[m], d) / A.tau;
+      if (j < n && j != i) {
+        lse_merge(ma, sa, s, 1.f);
+        const bool pos = b.ps ? (labj[m] != lab) : (labj[m] == lab);
+        if (pos) lse_merge(mp, sp, s, 1.f);
+      }
     }
-  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float m2 = __shfl_xor(ma, o, 64), s2 = __shfl_xor(sa, o, 64);
-    const float m3 = __shfl_xor(mp, o, 64), s3 = __shfl_xor(sp, o, 64);
-    lse_merge(ma, sa, m2, s2);
-    lse_merge(mp, sp, m3, s3);
-  }
-  if (lane == 0) {
-    b.lse[i] = (sa > 0.f) ? ma + logf(sa) : -INFINITY;
-    b.lse[n + i] = (sp > 0.f) ? mp + logf(sp) : -INFINITY;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(ma, o, 64), s2 = __shfl_xor(sa, o, 64);
+      const float m3 = __shfl_xor(mp, o, 64), s3 = __shfl_xor(sp, o, 64);
+      lse_merge(ma, sa, m2, s2);
+      lse_merge(mp, sp, m3, s3);
+    }
+    if (lane == 0) {
+      b.lse[i] = (sa > 0.f) ? ma + logf(sa) : -INFINITY;
+      b.lse[n + i] = (sp > 0.f) ? mp + logf(sp) : -INFINITY;
+    }
   }
 }
 
@@ -690,16 +696,13 @@ __device__ __forceinline__ void ntxent_grad_reg_body(const NtArgs& A, const int 
   const Branch& b = A.br[by];
   const int n = A.n, d = A.d;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int i = bx * A.rpb + w, ic = i < n ? i : 0;
-  // every load of the pair loop first (their latency overlaps the finite-row count and its barriers)
-  float mi[DM], mj[JM][DM], laj[JM], lpj[JM];
+  // every column load first (their latency overlaps the finite-row count and its barriers); the columns are the
+  // same for every row of the workgroup
+  float mj[JM][DM], laj[JM], lpj[JM];
   long long labj[JM];
-  ntr_row<DM>(b.mu + (size_t)ic * b.ld, d, mi);
-  const long long lab = A.label[ic];
-  const float la_i = b.lse[ic], lp_i = b.lse[n + ic];
 #pragma unroll
   for (int m = 0; m < JM; ++m) {
-    const int j = lane + 64 * m, jc = j < n ? j : ic;
+    const int j = lane + 64 * m, jc = j < n ? j : 0;
     ntr_row<DM>(b.mu + (size_t)jc * b.ld, d, mj[m]);
     labj[m] = A.label[jc];
     laj[m] = b.lse[jc];
@@ -720,47 +723,54 @@ __device__ __forceinline__ void ntxent_grad_reg_body(const NtArgs& A, const int 
     const double tot = block_sum<256>(lsum, dscratch);
     if (threadIdx.x == 0 && b.loss_out) b.loss_out[0] = (nf > 0.f) ? (float)(tot / (double)nf) : NAN;
   }
-  if (!b.dmu || i >= n) return;
+  if (!b.dmu) return;
   const float gup = b.gmul * (b.gscale ? b.gscale[0] : 1.0f);
   const float c = (nf > 0.f) ? gup / (nf * A.tau) : 0.f;
-  float rawi;
-  const float ni = ntr_unit<DM>(mi, d, &rawi);
 #pragma unroll
   for (int m = 0; m < JM; ++m) ntr_unit<DM>(mj[m], d);
-  const bool clamped_i = !(rawi > 1e-8f);
-  const bool fin_i = isfinite(la_i - lp_i);
-  float gm[DM];
+  const int iend = min(n, (bx + 1) * A.rpb);
+  for (int i = bx * A.rpb + w; i < iend; i += 4) {
+    float mi[DM];
+    ntr_row<DM>(b.mu + (size_t)i * b.ld, d, mi);
+    const long long lab = A.label[i];
+    const float la_i = b.lse[i], lp_i = b.lse[n + i];
+    float rawi;
+    const float ni = ntr_unit<DM>(mi, d, &rawi);
+    const bool clamped_i = !(rawi > 1e-8f);
+    const bool fin_i = isfinite(la_i - lp_i);
+    float gm[DM];
 #pragma unroll
-  for (int k = 0; k < DM; ++k) gm[k] = 0.f;
+    for (int k = 0; k < DM; ++k) gm[k] = 0.f;
 #pragma unroll
-  for (int m = 0; m < JM; ++m) {
-    const int j = lane + 64 * m;
-    const float S = dot_u<DM>(mi, mj[m], d);
-    const float s = S / A.tau;
-    const bool pos = b.ps ? (labj[m] != lab) : (labj[m] == lab);
-    const bool fin_j = isfinite(laj[m] - lpj[m]);
-    float G = 0.f;
-    if (fin_i) G += c * (expf(s - la_i) - (pos ? expf(s - lp_i) : 0.f));
-    if (fin_j) G += c * (expf(s - laj[m]) - (pos ? expf(s - lpj[m]) : 0.f));
-    if (j < n && j != i && G != 0.f) {
+    for (int m = 0; m < JM; ++m) {
+      const int j = lane + 64 * m;
+      const float S = dot_u<DM>(mi, mj[m], d);
+      const float s = S / A.tau;
+      const bool pos = b.ps ? (labj[m] != lab) : (labj[m] == lab);
+      const bool fin_j = isfinite(laj[m] - lpj[m]);
+      float G = 0.f;
+      if (fin_i) G += c * (expf(s - la_i) - (pos ? expf(s - lp_i) : 0.f));
+      if (fin_j) G += c * (expf(s - laj[m]) - (pos ? expf(s - lpj[m]) : 0.f));
+      if (j < n && j != i && G != 0.f) {
 #pragma unroll
-      for (int k = 0; k < DM; ++k)
-        if (k < d) gm[k] += G * (clamped_i ? mj[m][k] : (mj[m][k] - S * mi[k]));
+        for (int k = 0; k < DM; ++k)
+          if (k < d) gm[k] += G * (clamped_i ? mj[m][k] : (mj[m][k] - S * mi[k]));
+      }
     }
-  }
 #pragma unroll
-  for (int k = 0; k < DM; ++k)
-    if (k < d) gm[k] = wave_sum(gm[k]) / ni;
-  float om = 0.f;
+    for (int k = 0; k < DM; ++k)
+      if (k < d) gm[k] = wave_sum(gm[k]) / ni;
+    float om = 0.f;
 #pragma unroll
-  for (int k = 0; k < DM; ++k)
-    if (k == lane) om = gm[k];
-  if (lane < d) {
-    float* pm = b.dmu + (size_t)i * b.gld + lane;
-    *pm = A.accumulate ? *pm + om : om;
-    if (b.dlv) {
-      float* pl = b.dlv + (size_t)i * b.gld + lane;
-      *pl = A.accumulate ? *pl + 0.f : 0.f;  // (the LDS kernel adds its zero logvar gradient)
+    for (int k = 0; k < DM; ++k)
+      if (k == lane) om = gm[k];
+    if (lane < d) {
+      float* pm = b.dmu + (size_t)i * b.gld + lane;
+      *pm = A.accumulate ? *pm + om : om;
+      if (b.dlv) {
+        float* pl = b.dlv + (size_t)i * b.gld + lane;
+        *pl = A.accumulate ? *pl + 0.f : 0.f;  // (the LDS kernel adds its zero logvar gradient)
+      }
     }
   }
 }
