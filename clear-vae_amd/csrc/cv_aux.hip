@@ -86,7 +86,7 @@ int direct_aux_launch(const int* dkey, const direct::DArgs& da, dim3 dgrid, size
   const NtArgs& pa = g_aux.a;
   if ((pa.with_combine && g_aux.phase != 0) || pa.d > 8 || pa.n > NT_MAXN) return -1;
   const int dm = 8;
-  const int reg = ntxent_reg_ok(pa, pa.nbr) ? 1 : 0;
+  const int reg = (pa.d <= 8 && ntxent_reg_ok(pa, pa.nbr)) ? 1 : 0;  // (the DM = 8 instantiations below)
   const void* fn = nullptr;
   for (const Ent& e : k_aux) {
     bool ok = e.phase == g_aux.phase && e.dm == dm && e.reg == reg;

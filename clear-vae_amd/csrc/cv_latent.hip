@@ -121,6 +121,60 @@ __global__ __launch_bounds__(1024) void combine_kernel(const CombineArgs C) {
   combine_body<1024>(C, scratch);
 }
 
+// The combine over several workgroups (one batch of 8 elements per thread each): the element-wise d(heads) terms
+// are the one-workgroup kernel's, the KL sums meet in two fp64 accumulators (device atomics, then an arrival count);
+// the last workgroup to arrive writes the losses and resets the accumulators and the count for the next launch.
+// A single workgroup walking n x 2d elements in 8-element batches was a chain of dependent round trips on the
+// step's critical path (MNIST 10 us, VAE64 17 us).  CV_COMBINE_WG=0: the one-workgroup kernel (A/B).
+__device__ double g_comb_acc[2];
+__device__ unsigned g_comb_ticket;
+constexpr int CMB_NT = 256;
+__global__ __launch_bounds__(CMB_NT) void combine_multi_kernel(const CombineArgs C) {
+  __shared__ double scratch[16];
+  __shared__ int last;
+  double kc, ks;
+  const float w = combine_sums<CMB_NT>(C, blockIdx.x * CMB_NT * 8, gridDim.x * CMB_NT * 8, scratch, &kc, &ks);
+  if (threadIdx.x == 0) {
+    atomic_add_f64(g_comb_acc, kc);
+    atomic_add_f64(g_comb_acc + 1, ks);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(&g_comb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const double a = __hip_atomic_load(g_comb_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const double b = __hip_atomic_load(g_comb_acc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g_comb_acc, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g_comb_acc + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&g_comb_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (C.rec_in) {
+        double r = 0.0;
+        for (int q = 0; q < CV_REC_REPL; ++q) r += C.rec_in[q];
+        C.losses[0] = (float)r;
+      }
+      C.losses[1] = (float)(-0.5 * a / (double)C.n);
+      C.losses[2] = (float)(-0.5 * b / (double)C.n);
+      C.losses[7] = w;
+    }
+  }
+}
+
+static void combine_launch(const CombineArgs& C, hipStream_t st) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("CV_COMBINE_WG");
+    mode = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  const long total = (long)C.n * 2 * C.d;
+  long g = (total + CMB_NT * 8 - 1) / (CMB_NT * 8);
+  if (g > 64) g = 64;
+  if (!mode || g < 2) {
+    hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, st, C);
+    return;
+  }
+  note_launch((const void*)combine_multi_kernel);
+  hipLaunchKernelGGL(combine_multi_kernel, dim3((unsigned)g), dim3(CMB_NT), 0, st, C);
+}
+
 // ---------------------------------------------------------------- reconstruction MSE (autograd path)
 __global__ __launch_bounds__(1024) void mse_kernel(const float* __restrict__ xh, const float* __restrict__ x, long total,
                                                    int n, float* rec_out, double* acc) {
@@ -581,7 +635,8 @@ static int ntxent_launch_lds(const NtArgs& a, int nbr, bool rows, hipStream_t st
   if (ntxent_reg_ok(a, nbr)) {
     arg.rpb = ntr_rows();
     const dim3 grid(cdiv(a.n, arg.rpb), nbr + ((rows && a.with_combine) ? 1 : 0));
-    const void* kr = rows ? (const void*)ntxent_rows_reg_kernel<8, NTR_JM> : (const void*)ntxent_grad_reg_kernel<8, NTR_JM>;
+    const void* kr = a.d <= 8 ? (rows ? (const void*)ntxent_rows_reg_kernel<8, NTR_JM> : (const void*)ntxent_grad_reg_kernel<8, NTR_JM>)
+                              : (rows ? (const void*)ntxent_rows_reg_kernel<32, 4> : (const void*)ntxent_grad_reg_kernel<32, 4>);
     void* params[] = {&arg};
     note_launch(kr);
     if (hipLaunchKernel(kr, grid, dim3(256), params, 16 * sizeof(double), st) != hipSuccess) {
@@ -698,7 +753,7 @@ extern "C" int cv_latent_combine(const float* heads, const float* z, const float
   clear_error();
   CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine: bad args");
   const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 0};
-  hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), C);
+  combine_launch(C, S(stream));
   CV_LAUNCH_CHECK("latent_combine");
   return 0;
 }
@@ -709,7 +764,7 @@ extern "C" int cv_latent_combine_acc(const float* heads, const float* z, const f
   clear_error();
   CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine_acc: bad args");
   const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 1};
-  hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, S(stream), C);
+  combine_launch(C, S(stream));
   CV_LAUNCH_CHECK("latent_combine_acc");
   return 0;
 }

@@ -21,8 +21,12 @@ struct CombineArgs {
   int accumulate;  // 1: dheads += (the contrastive / MI terms are already in it)
 };
 
+// The element-wise part of the combine over the batches that start at `first` + threadIdx.x and advance by `step`
+// (one workgroup: 0, NTH * 8; several: a contiguous chunk each), with the workgroup's fp64 KL sums in *kc / *ks;
+// returns the annealer weight.
 template <int NTH>
-__device__ __forceinline__ void combine_body(const CombineArgs& C, double* scratch) {
+__device__ __forceinline__ float combine_sums(const CombineArgs& C, int first, int step, double* scratch, double* kc_out,
+                                              double* ks_out) {
   const float* __restrict__ heads = C.heads;
   const float* __restrict__ z = C.z;
   const float* __restrict__ dz = C.dz;
@@ -40,7 +44,7 @@ __device__ __forceinline__ void combine_body(const CombineArgs& C, double* scrat
   // latencies per thread at VAE64 bs=256).  Each thread still visits e = t, t + NTH, ... in order, so
   // the fp64 KL sums are bit-identical to the element-at-a-time loop.
   constexpr int U = 8;
-  for (int base = threadIdx.x; base < total; base += NTH * U) {
+  for (int base = first + threadIdx.x; base < total; base += step) {
     float m[U], l[U], g[U], zz[U];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
@@ -80,8 +84,16 @@ __device__ __forceinline__ void combine_body(const CombineArgs& C, double* scrat
       dheads[(size_t)r * 4 * d + (blk + 1) * d + k] = C.accumulate ? ol[q] + vl : vl;
     }
   }
-  const double kc = block_sum<NTH>(sc, scratch);
-  const double ks = block_sum<NTH>(ss, scratch);
+  *kc_out = block_sum<NTH>(sc, scratch);
+  *ks_out = block_sum<NTH>(ss, scratch);
+  return w;
+}
+
+template <int NTH>
+__device__ __forceinline__ void combine_body(const CombineArgs& C, double* scratch) {
+  double kc, ks;
+  const float w = combine_sums<NTH>(C, 0, NTH * 8, scratch, &kc, &ks);
+  const int n = C.n;
   if (threadIdx.x == 0) {
     if (C.rec_in) {
       double r = 0.0;
@@ -595,17 +607,17 @@ __device__ __forceinline__ void ntxent_grad_lds_body(const NtArgs& A, const int 
 }
 
 // Register-resident variants for small batches (cosine similarity, n <= 64 * JM, d <= DM, 16-byte rows: MNIST's
-// bs = 512, d = 8).  The LDS kernels above stage the whole branch per workgroup (two dependent HBM/L2 round trips,
+// bs = 512, d = 8; VAE64's bs <= 256, d = 32).  The LDS kernels above stage the whole branch per workgroup (two dependent HBM/L2 round trips,
 // three barriers and two LDS passes before the first pair), then walk one row per wave: at these sizes the staging
 // is the kernel.  Here every lane requests its JM columns (rows j = lane + 64 m as float4s, the label, and for the
 // gradients the two log-sum-exps) and the wave's own row in ONE batch of loads, normalises in registers and runs
 // the same pair loop.  The arithmetic, and its order, is the LDS kernels' (unit vectors = row / max(|row|, 1e-8),
 // the same dot products, the same per-lane merge order j ascending, the same shuffle tree and 1/n_i placement), so
 // the results are bit-identical to them (tests/test_gpu_ntxent_reg.py).
-constexpr int NTR_JM = 8;
+constexpr int NTR_JM = 8;  // columns per lane of the d <= 8 form (n <= 512); the d <= 32 form takes 4 (n <= 256)
 int ntr_rows();  // rows per 256-thread workgroup of the register variants (cv_latent.hip; CV_NT_ROWS A/B)
 __host__ __device__ inline bool ntr_fits(int n, int d, int sim) {
-  return sim == CV_SIM_COSINE && n <= 64 * NTR_JM && d <= 8 && d % 4 == 0;
+  return sim == CV_SIM_COSINE && d % 4 == 0 && ((n <= 64 * NTR_JM && d <= 8) || (n <= 256 && d <= 32));
 }
 
 template <int DM>

@@ -1,12 +1,12 @@
-"""The register-resident NT-Xent variants (csrc/cv_ntxent.hpp ntxent_*_reg_body: cosine similarity, n <= 512,
-d <= 8 in 16-byte rows — MNIST's bs = 512, z = 16) against the LDS-staged kernels they replace (cv_debug_nt_reg(0)).
+"""The register-resident NT-Xent variants (csrc/cv_ntxent.hpp ntxent_*_reg_body: cosine similarity, n <= 512 with
+d <= 8 or n <= 256 with d <= 32, in 16-byte rows — MNIST's bs = 512, z = 16; VAE64's bs <= 256, z = 64) against the LDS-staged kernels they replace (cv_debug_nt_reg(0)).
 Reference: losses.py:98-137 (contrastive_loss / snn_loss through the cosine similarity, losses.py:70-76).
 
 Both variants do the same arithmetic in the same order, so the row log-sum-exps, the losses and the gradients must be
 BIT-identical: batches at, below and not a multiple of the tile (512, 300, 64, 5), d = 8 and 4, the two positive-set
 rules (ps = 1: different label, ps = 0: same label), accumulate on and off, the heads' strided layout (ld = 4d), a
 zero row (the clamped-norm path of the gradient) and rows without positives (non-finite rows, dropped from the
-mean).  The fused step through the reg path is held to the fp64 oracle by test_gpu_aux.py / test_gpu_parity.py."""
+mean); VAE64's d = 32 at n = 256 / 128 and d = 16.  The fused step through the reg path is held to the fp64 oracle by test_gpu_aux.py / test_gpu_parity.py."""
 
 import numpy as np
 import pytest
@@ -37,8 +37,8 @@ def _run(reg, mu_all, lab, n, d, ps, accumulate, ld, seed_grad):
     return lse.cpu(), loss.cpu(), dmu.cpu(), dlv.cpu()
 
 
-@pytest.mark.parametrize("n", [512, 300, 64, 5])
-@pytest.mark.parametrize("d", [8, 4])
+@pytest.mark.parametrize("n,d", [(512, 8), (300, 8), (64, 8), (5, 8), (512, 4), (64, 4), (256, 32), (128, 32),
+                                 (100, 16), (7, 32)])
 @pytest.mark.parametrize("ps", [1, 0])
 @pytest.mark.parametrize("accumulate", [0, 1])
 def test_reg_variant_bit_identical(n, d, ps, accumulate):
