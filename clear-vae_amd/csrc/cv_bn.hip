@@ -506,9 +506,12 @@ struct StepRedArgs {
   int nprod;  // blocks that reduce the deferred segments (grid-stride over blk0[nd] segments)
 };
 #ifndef CV_SR_E
-#define CV_SR_E 128
+#define CV_SR_E 64
 #endif
-constexpr int SR_E = CV_SR_E;      // partial-tile elements per block: 256-byte row segments
+// partial-tile elements per block (256-byte row segments), each summed by SR_G thread groups over every SR_G-th
+// split.  64 (4 groups): MNIST step 0.4972 -> 0.4942 ms (the reduction 20.5 -> 17.6 us in-step), CelebA 2.1216 ->
+// 2.1179 ms against 128 (2 groups); 32 (8 groups) lost on CelebA (2.137 ms).  -DCV_SR_E= rebuilds (A/B).
+constexpr int SR_E = CV_SR_E;
 constexpr int SR_G = 256 / SR_E;   // split groups per element (each thread sums every SR_G-th split)
 
 // torch.optim.Adam (foreach) on one element of the arena, constants from adam_consts

@@ -235,8 +235,9 @@ def _chain_torch(dheads, heads, z, dz, d):
 @pytest.mark.parametrize("n,C,pix,J", HEADS)
 def test_heads_backward_chain(n, C, pix, J):
     """cv_heads_backward_chain (the decoder chain term added while dheads is staged, engine LATENT_CHAIN) is
-    cv_heads_backward of dheads + that term: bit-identical outputs (the BN backward sums, fp64 atomics of several
-    workgroups, to 1e-12), dheads left as it was, losses[0] = the rec replicas' sum."""
+    cv_heads_backward of dheads + that term: bit-identical d(input) (the weight / bias gradients to 1e-6 and the BN
+    backward sums, fp64 atomics of several workgroups, to 1e-12: summation order only), dheads left as it was,
+    losses[0] = the rec replicas' sum."""
     from cvhip import _lib
 
     dev = torch.device("cuda")
@@ -280,8 +281,11 @@ def test_heads_backward_chain(n, C, pix, J):
         torch.cuda.synchronize()
         assert torch.equal(dheads, before)
         outs.append((gin.cpu(), gw.cpu(), gb.cpu(), gstat.cpu()))
-    for a, b, name in zip(outs[0][:3], outs[1][:3], ("gin", "gw", "gb")):
-        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), (name, (a - b).abs().max())
+    assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32)), (outs[0][0] - outs[1][0]).abs().max()
+    # (gw / gb: the plain launch splits the rows of a large batch over two workgroups whose sums meet in atomics, the
+    # chained one does not: the same sums in another order)
+    for a, b, name in zip(outs[0][1:3], outs[1][1:3], ("gw", "gb")):
+        assert _rel(a, b) < 1e-6, (name, _rel(a, b))
     assert _rel(outs[0][3], outs[1][3]) < 1e-12
     r = 0.0
     for v in rec.cpu().tolist():  # (the kernel's order)
