@@ -758,6 +758,15 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    int64_t* aux) {
   __shared__ float cst[8];
   __shared__ int flag;
+  // the first float4 of every thread is requested before thread 0's constants (two fp64 pow) and the barrier
+  const long n4 = numel >> 2, i0 = (long)blockIdx.x * 256 + threadIdx.x;
+  float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), p0 = g0, m0 = g0, v0 = g0;
+  if (i0 < n4) {
+    g0 = reinterpret_cast<const float4*>(gr)[i0];
+    p0 = reinterpret_cast<const float4*>(p)[i0];
+    m0 = reinterpret_cast<const float4*>(m)[i0];
+    v0 = reinterpret_cast<const float4*>(v)[i0];
+  }
   if (threadIdx.x == 0) {
     const long t_step = step[0] + 1;
     const double b1 = hyper[1], b2 = hyper[2];
@@ -775,7 +784,6 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   __syncthreads();
   const float step_size = cst[0], bc2s = cst[1], omb1 = cst[2], omb2 = cst[3], b2f = cst[4], eps = cst[5];
   const float wd = cst[6], gs = cst[7];
-  const long n4 = numel >> 2;
   auto upd = [&](float g, float pp, float& mm, float& vv) -> float {
     g *= gs;
     if (wd != 0.f) g = g + wd * pp;
@@ -784,11 +792,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     const float den = sqrtf(vv) / bc2s + eps;
     return pp + step_size * (mm / den);
   };
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    const float4 g4 = reinterpret_cast<const float4*>(gr)[i];
-    float4 p4 = reinterpret_cast<float4*>(p)[i];
-    float4 m4 = reinterpret_cast<float4*>(m)[i];
-    float4 v4 = reinterpret_cast<float4*>(v)[i];
+  for (long i = i0; i < n4; i += (long)gridDim.x * 256) {
+    const bool first = i == i0;
+    const float4 g4 = first ? g0 : reinterpret_cast<const float4*>(gr)[i];
+    float4 p4 = first ? p0 : reinterpret_cast<float4*>(p)[i];
+    float4 m4 = first ? m0 : reinterpret_cast<float4*>(m)[i];
+    float4 v4 = first ? v0 : reinterpret_cast<float4*>(v)[i];
     p4.x = upd(g4.x, p4.x, m4.x, v4.x);
     p4.y = upd(g4.y, p4.y, m4.y, v4.y);
     p4.z = upd(g4.z, p4.z, m4.z, v4.z);
