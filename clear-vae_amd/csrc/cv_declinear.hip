@@ -616,6 +616,7 @@ struct HeadsFwdArgs {
   uint64_t* offset;
   float* z;             // [n][2d]
   int n, d, J, F, ch, ngrp, jt;  // jt: 16-column tiles per group (1: d = 8, 2: d % 16 == 0)
+  int rows;                      // rows per workgroup: 16 (one MFMA row tile), or 8 (the tile's upper half idle)
 };
 
 constexpr int HF_NT = 1024;
@@ -628,7 +629,7 @@ __global__ __launch_bounds__(HF_NT) void heads_fwd_kernel(const HeadsFwdArgs A) 
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
   const int n = A.n, F = A.F, C = A.ch, d = A.d, J = A.J;
   const int rb = blockIdx.x / A.ngrp, gi = blockIdx.x - rb * A.ngrp;
-  const int row0 = 16 * rb;
+  const int row0 = A.rows * rb;
   // the group's columns: tile 0 (and tile 1, the logvar partner)
   int c0[2];
   if (JT == 1) {
@@ -659,7 +660,8 @@ __global__ __launch_bounds__(HF_NT) void heads_fwd_kernel(const HeadsFwdArgs A) 
   const int kper = F / NWV;  // (host: F % (16 * NWV) == 0)
   const int kb = w * kper;
   const int row = row0 + lr;
-  const float* yr = A.y + (size_t)(row < n ? row : 0) * F;
+  const bool live = lr < A.rows && row < n;
+  const float* yr = A.y + (size_t)(live ? row : 0) * F;
   f32x4 acc[JT];
 #pragma unroll
   for (int j = 0; j < JT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -684,7 +686,7 @@ __global__ __launch_bounds__(HF_NT) void heads_fwd_kernel(const HeadsFwdArgs A) 
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         a[s] = fmaxf(fmaf(a[s] - cst[1][c + s], cst[0][c + s], cst[2][c + s]), 0.f);
-        if (row >= n) a[s] = 0.f;
+        if (!live) a[s] = 0.f;
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -705,7 +707,7 @@ __global__ __launch_bounds__(HF_NT) void heads_fwd_kernel(const HeadsFwdArgs A) 
     const int col = c0[j] + cc;
     v += A.bias ? A.bias[col] : 0.f;
     hs[rr][16 * j + cc] = v;
-    if (row0 + rr < n) A.heads[(size_t)(row0 + rr) * J + col] = v;
+    if (rr < A.rows && row0 + rr < n) A.heads[(size_t)(row0 + rr) * J + col] = v;
   }
   if (!A.z) return;
   __syncthreads();
@@ -713,7 +715,7 @@ __global__ __launch_bounds__(HF_NT) void heads_fwd_kernel(const HeadsFwdArgs A) 
   const int half = (JT == 1) ? gi : (c0[0] >= 2 * d ? 1 : 0);  // 0: z_c, 1: z_s
   const int lat0 = (JT == 1) ? 0 : c0[0] - half * 2 * d;      // first latent of the group within its half
   const int nl = (JT == 1) ? d : 16;                           // latents of the group
-  for (int e = 2 * t; e < 16 * nl; e += 2 * HF_NT) {
+  for (int e = 2 * t; e < A.rows * nl; e += 2 * HF_NT) {
     const int rr = e / nl, m = e - rr * nl;  // (nl even: a pair stays in one row)
     const int grow = row0 + rr;
     if (grow >= n) continue;
@@ -981,7 +983,16 @@ extern "C" int cv_heads_forward(const cv_linear* g, const float* y, const cv_bn*
   a.ch = ch;
   a.jt = d == 8 ? 1 : 2;
   a.ngrp = d == 8 ? 2 : 2 * (d / 16);
-  const dim3 grid(cdiv(g->n, 16) * a.ngrp);
+  // CV_HEADS_FWD_ROWS=8 (A/B): 8-row workgroups, twice the grid where 16-row ones leave most CUs idle (MNIST bs =
+  // 512 and VAE64 bs = 256: 64 workgroups) — measured neutral (MNIST 0.4953 vs 0.4942 ms, CelebA 2.1267 vs
+  // 2.1271 ms: the per-workgroup constants and weight loads, not the row count, set its length), so 16
+  static int rows_ovr = -2;
+  if (rows_ovr == -2) {
+    const char* e = getenv("CV_HEADS_FWD_ROWS");
+    rows_ovr = e ? atoi(e) : -1;
+  }
+  a.rows = rows_ovr == 8 ? 8 : 16;
+  const dim3 grid(cdiv(g->n, a.rows) * a.ngrp);
   if (a.jt == 1) hipLaunchKernelGGL(heads_fwd_kernel<1>, grid, dim3(HF_NT), 0, S(stream), a);
   else hipLaunchKernelGGL(heads_fwd_kernel<2>, grid, dim3(HF_NT), 0, S(stream), a);
   CV_LAUNCH_CHECK("heads_forward");
