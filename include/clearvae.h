@@ -362,6 +362,8 @@ int cv_latent_combine(const float* heads, const float* z, const float* dz, int n
 int cv_latent_combine_acc(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                           float loc, float scale, const int64_t* anneal_step, const double* rec_in,
                           float* dheads, float* losses, cv_stream_t stream);
+/* (Both combine entries run over several workgroups when n x 2d >= 4096 elements, their KL sums meeting in a
+ * per-device accumulator: two combine launches on one device must not overlap in time — e.g. on two streams.) */
 
 /* reconstruction term (losses.py:45-47) for the autograd path: rec = mean_n sum (xhat - x)^2;
  * work: one zeroed fp64 word.  dxhat != NULL: dxhat = gscale[0] * 2 (xhat - x) / n. */
