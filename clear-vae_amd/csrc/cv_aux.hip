@@ -16,7 +16,6 @@
 
 namespace cv {
 thread_local AuxPend g_aux;
-bool ntxent_reg_ok(const NtArgs& a, int nbr);  // (cv_latent.hip)
 
 namespace aux {
 
@@ -77,6 +76,9 @@ static int enabled() {
 }
 
 }  // namespace aux
+
+bool aux_enabled() { return aux::enabled() != 0; }
+void aux_count_merged() { ++aux::g_merged; }
 
 // the pending NT-Xent phase with this direct launch as one grid: 0 / 2 (launched / launch error), -1 (not served:
 // the caller launches the direct kernel alone and the phase stays queued)

@@ -7,6 +7,7 @@
 //   vae_loss reconstruction term: mean_n sum_{chw} (xhat - x)^2                 losses.py:36-47
 //   decoder Linear(z, 2048) -> BatchNorm1d(2048) -> ReLU backward               vae.py:33-35
 #include "cv_common.hpp"
+#include "cv_ntxent.hpp"
 
 namespace cv {
 
@@ -106,17 +107,35 @@ __global__ __launch_bounds__(256) void output_fwd_kernel(const cv_bn b, const fl
 // dv store (NHWC) is coalesced; x / xhat are NCHW.
 // grid-stride over element batches of OL_U per thread: all loads of a batch are issued first
 constexpr int OL_U = 4;
-__global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const float* __restrict__ y,
-                                                          const float* __restrict__ x, int n, int c, int hw,
-                                                          const FDiv fc, const FDiv fhw,
-                                                          float* __restrict__ xhat, double* rec_out,
-                                                          float* __restrict__ dv, double* gstat,
-                                                          const float* rec_scale) {
+struct OutLossArgs {
+  cv_bn b;
+  const float* y;
+  const float* x;
+  int n, c, hw;
+  FDiv fc, fhw;
+  float* xhat;
+  double* rec_out;
+  float* dv;
+  double* gstat;
+  const float* rec_scale;
+};
+// workgroup bx of gx (a grid of its own, or its share of an auxiliary-role grid)
+__device__ __forceinline__ void output_loss_body(const OutLossArgs& A, const int bx, const int gx) {
+  const cv_bn& b = A.b;
+  const float* __restrict__ y = A.y;
+  const float* __restrict__ x = A.x;
+  const int n = A.n, c = A.c, hw = A.hw;
+  const FDiv fc = A.fc, fhw = A.fhw;
+  float* __restrict__ xhat = A.xhat;
+  double* rec_out = A.rec_out;
+  float* __restrict__ dv = A.dv;
+  double* gstat = A.gstat;
+  const float* rec_scale = A.rec_scale;
   __shared__ BnFwdC k[OUT_MAXC];
   __shared__ double red[4][1 + 2 * OUT_MAXC];
   __shared__ double scratch[4 * 256];
   const int total = n * c * hw;
-  const int base0 = blockIdx.x * 256 * OL_U;
+  const int base0 = bx * 256 * OL_U;
   float yv[OL_U], xv[OL_U];
   int nchw[OL_U], chs[OL_U];
   auto load = [&](int base) {
@@ -146,7 +165,7 @@ __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const f
   float s1[OUT_MAXC], s2[OUT_MAXC];
 #pragma unroll
   for (int j = 0; j < OUT_MAXC; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  for (int base = base0; base < total; base += gridDim.x * 256 * OL_U) {
+  for (int base = base0; base < total; base += gx * 256 * OL_U) {
     if (base != base0) load(base);
 #pragma unroll
     for (int u = 0; u < OL_U; ++u) {
@@ -184,9 +203,9 @@ __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const f
   __syncthreads();
   if (threadIdx.x == 0) {
     double r = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-    atomic_add_f64(rec_out + blockIdx.x % CV_REC_REPL, r / (double)n);
+    atomic_add_f64(rec_out + bx % CV_REC_REPL, r / (double)n);
     if (dv) {
-      const int repl = blockIdx.x % CV_STAT_REPL(c);
+      const int repl = bx % CV_STAT_REPL(c);
       for (int j = 0; j < c; ++j) {
         const double a = red[0][1 + j] + red[1][1 + j] + red[2][1 + j] + red[3][1 + j];
         const double bb = red[0][1 + OUT_MAXC + j] + red[1][1 + OUT_MAXC + j] + red[2][1 + OUT_MAXC + j] +
@@ -196,6 +215,29 @@ __global__ __launch_bounds__(256) void output_loss_kernel(const cv_bn b, const f
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void output_loss_kernel(const OutLossArgs A) { output_loss_body(A, blockIdx.x, gridDim.x); }
+
+// The output loss with a queued NT-Xent gradient phase as extra workgroups of the same grid (cv_ntxent_aux; the
+// fused step queues it before the last ConvTranspose2d, whose grid the image-side scatter fills): the roles
+// alternate over the first 2 x min(nd, na) workgroups, as in cv_aux.hip.  Register-resident phase (d <= 8) only.
+struct OlAuxMap {
+  int nd, na, agx;
+};
+__global__ __launch_bounds__(256) void output_loss_aux_kernel(const OutLossArgs A, const NtArgs P, const OlAuxMap m) {
+  const int v = blockIdx.x;
+  const int k2 = m.nd < m.na ? m.nd : m.na;
+  int role, idx;
+  if (v < 2 * k2) {
+    role = v & 1;
+    idx = v >> 1;
+  } else {
+    role = m.nd > m.na ? 0 : 1;
+    idx = k2 + (v - 2 * k2);
+  }
+  if (role == 0) output_loss_body(A, idx, m.nd);
+  else ntxent_grad_reg_body<8, NTR_JM>(P, idx % m.agx, idx / m.agx);
 }
 
 __global__ __launch_bounds__(256) void output_bwd_kernel(const cv_bn b, const float* __restrict__ y,
@@ -920,8 +962,22 @@ extern "C" int cv_output_loss(const cv_bn* bn, const float* y, const float* x, i
   CV_REQUIRE((long)n * c * hw < (1L << 31), "output_loss: tensor too large");
   long g = ((long)n * c * hw + 256 * OL_U - 1) / (256 * OL_U);
   if (g > 512) g = 512;
-  hipLaunchKernelGGL(output_loss_kernel, dim3((int)g), dim3(256), 0, S(stream), *bn, y, x, n, c, hw, FDiv::make(c),
-                     FDiv::make(hw), xhat, rec_out, dv_out, gstat_out, rec_scale);
+  const OutLossArgs A{*bn, y, x, n, c, hw, FDiv::make(c), FDiv::make(hw), xhat, rec_out, dv_out, gstat_out, rec_scale};
+  // a queued NT-Xent gradient phase rides in this grid where served (cv_ntxent_aux; else it stays queued for its
+  // flush)
+  if (g_aux.set && g_aux.phase == 1 && aux_enabled() && g_aux.a.d <= 8 && !g_aux.a.with_combine &&
+      ntxent_reg_ok(g_aux.a, g_aux.a.nbr)) {
+    const NtArgs P = g_aux.a;
+    const int agx = (P.n + P.rpb - 1) / P.rpb;
+    const OlAuxMap m{(int)g, agx * P.nbr, agx};
+    g_aux.set = 0;
+    note_launch((const void*)output_loss_aux_kernel);
+    hipLaunchKernelGGL(output_loss_aux_kernel, dim3((unsigned)(m.nd + m.na)), dim3(256), 0, S(stream), A, P, m);
+    aux_count_merged();
+    CV_LAUNCH_CHECK("output_loss + NT-Xent");
+    return 0;
+  }
+  hipLaunchKernelGGL(output_loss_kernel, dim3((int)g), dim3(256), 0, S(stream), A);
   CV_LAUNCH_CHECK("output_loss");
   return 0;
 }

@@ -794,5 +794,8 @@ struct AuxPend {
   NtArgs a;
 };
 extern thread_local AuxPend g_aux;
+bool ntxent_reg_ok(const NtArgs& a, int nbr);  // (cv_latent.hip)
+bool aux_enabled();                            // (cv_aux.hip: CV_AUX / cv_debug_aux)
+void aux_count_merged();                       // (cv_aux.hip: cv_debug_aux_count)
 
 }  // namespace cv

@@ -79,6 +79,11 @@ LATENT_SIDE = os.environ.get("CVHIP_LATENT_SIDE", "0") == "1"
 # decoder backward (cv_latent_combine_acc).  One stream, no graph edges; d(heads) is bit-identical (the same two adds
 # per element, in the other order).
 LATENT_AUX = os.environ.get("CVHIP_LATENT_AUX", "1") == "1"
+# CVHIP_LATENT_AUX_OUT=1 (A/B knob, off; with LATENT_AUX): the gradient phase is queued before the last decoder
+# conv instead of the second: the output-loss launch that follows the image-side scatter serves it (cv_output_loss),
+# and the second ConvTranspose2d's grid runs alone.  Measured (round 5, MNIST, two rounds): ConvT2 35.3 -> 27.5 us
+# in-step but the output call 22.1 -> 31.4 us, step 0.4960 -> 0.4966 ms — the phase costs ~9 us wherever it rides.
+LATENT_AUX_OUT = os.environ.get("CVHIP_LATENT_AUX_OUT", "0") == "1"
 
 # CVHIP_LATENT_CHAIN=1 (A/B knob, off; with LATENT_AUX): the latent combine split at its dependency.  Its KL part (losses
 # 1, 2, 7 and the KL gradient, written into the zeroed d(heads)) needs only the heads, so it rides as one more
@@ -405,7 +410,8 @@ class ClearStep:
                 f.keep += [gwork, gscale_rec]
             else:
                 ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp, aux=aux_args,
-                                   aux_combine=aux_comb)
+                                   aux_combine=aux_comb,
+                                   aux_at=(0, len(sp.dec) - 1) if LATENT_AUX_OUT else None)
                 if aux_nt:
                     f.keep.append(br_arr)
             # (the running statistics are folded at the end of the backward by cv_step_reduce)

@@ -783,11 +783,13 @@ class Workspace:
         return self.FUSED_HEADS and bool(_lib.lib().cv_heads_backward_supported(self.n, sp.F, C, 4 * sp.d))
 
     def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None,
-                        aux=None, aux_combine=None):
+                        aux=None, aux_combine=None, aux_at=None):
         """reparam = (eps, seed, offset): z is drawn from self.heads first (cv_reparam_forward, or inside the
         fused decoder-input launch); None: z is given.  aux: cv_ntxent_aux argument tuples, the i-th queued before
-        the i-th decoder conv (its phase rides in that launch where served) and flushed right after it;
-        aux_combine: cv_ntxent_aux_combine arguments attached to the first (the KL part of the latent combine)."""
+        the i-th decoder conv (its phase rides in that launch where served) and flushed right after it — or
+        before the decoder conv aux_at[i] (the last one: the output-loss call, whose loss launch serves a gradient
+        phase); aux_combine: cv_ntxent_aux_combine arguments attached to the first (the KL part of the latent
+        combine)."""
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
@@ -811,21 +813,25 @@ class Workspace:
         cur = self.ah
         last = sp.dec[-1]
         hw = last.h_out * last.w_out
+        at = {} if aux is None else {(aux_at[q] if aux_at is not None else q): q for q in range(len(aux))}
         for li, c in enumerate(sp.dec):
             g = c.geom(n)
             op = operand(cur) if li == 0 else operand(cur, XF_BNRELU, self.bn_dec[li - 1].cv(train))
             ep = ep_fwd(self.bn_dec[li]) if train else ep_none()
+            q = at.get(li)
+            if q is not None:
+                P.add("cv_ntxent_aux", *aux[q])
+                if q == 0 and aux_combine is not None:
+                    P.add("cv_ntxent_aux_combine", *aux_combine)
             if li == len(sp.dec) - 1 and output == "loss":  # the last ConvT and the output / loss seed together
                 assert train
                 P.add("cv_convt_output_loss", g, op, c.wfwd, c.mod.bias, self.y_dec[li], ep, self.bn_dec[-1].cv(True), x,
                       self.xhat, self.rec, self.g_dec[-1], self.bn_dec[-1].gstat, rec_scale)
+                if q is not None:
+                    P.add("cv_ntxent_aux_flush")
                 return
-            if aux is not None and li < len(aux):
-                P.add("cv_ntxent_aux", *aux[li])
-                if li == 0 and aux_combine is not None:
-                    P.add("cv_ntxent_aux_combine", *aux_combine)
             P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, self.y_dec[li], ep)
-            if aux is not None and li < len(aux):
+            if q is not None:
                 P.add("cv_ntxent_aux_flush")
             cur = self.y_dec[li]
         if output == "xhat":

@@ -12,7 +12,8 @@ with the previous schedule (cv_latent_step after the decoder backward):
 Also with the merge switched off in the library (cv_debug_aux(0)): the queued phases launch on their own at the
 flush points, same results.  Both with the combine split (LATENT_CHAIN, default: its KL part rides in the rows-phase
 grid, the decoder-chain part in the heads backward — d(heads) in memory then lacks the chain term, which the test
-adds from z / dz / heads) and with the one-launch combine after the decoder backward."""
+adds from z / dz / heads) and with the one-launch combine after the decoder backward; and with the gradient phase
+queued before the output-loss launch instead (LATENT_AUX_OUT, cv_output_loss serves it)."""
 
 import numpy as np
 import pytest
@@ -66,13 +67,20 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
-@pytest.mark.parametrize("chain", [True, False], ids=["chain", "combine-launch"])
+@pytest.mark.parametrize("chain,aux_out", [(True, False), (False, False), (False, True)],
+                         ids=["chain", "combine-launch", "grad-in-output-loss"])
 @pytest.mark.parametrize("aux_lib", [True, False], ids=["merged", "standalone-at-flush"])
-def test_aux_schedule_matches_latent_step(aux_lib, chain):
+def test_aux_schedule_matches_latent_step(aux_lib, chain, aux_out):
     from oracle import cpu_ref as R
+    from cvhip import engine
     from test_gpu_declinear import _chain_torch
 
-    new, inp = _run(True, aux_lib, chain)
+    prev = engine.LATENT_AUX_OUT
+    engine.LATENT_AUX_OUT = aux_out
+    try:
+        new, inp = _run(True, aux_lib, chain)
+    finally:
+        engine.LATENT_AUX_OUT = prev
     old, _ = _run(False, True)
     assert new["merged"] == (2 if aux_lib else 0), new["merged"]
     assert old["merged"] == 0
