@@ -654,8 +654,9 @@ struct PackArgs {
   int n;
   // the step's zeroed buffers (cv_pack_conv_weights_zero): the blockIdx.y == n slice clears them
   uint32_t* zp[8];
-  long zstart[9];  // prefix sums of 4-byte words
+  long zstart[9];  // prefix sums of 4-byte words (zvec: of 16-byte units)
   int zn;
+  int zvec;        // every zeroed buffer 16-byte aligned and sized: 16-byte stores
 };
 
 // blockIdx.y == a.n: zero the listed buffers (grid-stride over blockIdx.x)
@@ -664,7 +665,8 @@ __device__ __forceinline__ void pack_zero_slice(const PackArgs& a) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     int b = 0;
     while (b + 1 < a.zn && i >= a.zstart[b + 1]) ++b;
-    a.zp[b][i - a.zstart[b]] = 0u;
+    if (a.zvec) reinterpret_cast<uint4*>(a.zp[b])[i - a.zstart[b]] = make_uint4(0u, 0u, 0u, 0u);
+    else a.zp[b][i - a.zstart[b]] = 0u;
   }
 }
 // small layers: one destination element per thread, each destination walked in its own order
@@ -1473,12 +1475,14 @@ static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, con
   PackArgs a;
   memset(&a, 0, sizeof(a));
   a.zn = zcount;
+  a.zvec = 1;
   for (int i = 0; i < zcount; ++i) {
     CV_REQUIRE(zptrs[i] && zbytes[i] % 4 == 0 && ((uintptr_t)zptrs[i] & 3) == 0,
                "pack_conv_weights: zero buffer %d not 4-byte granular", i);
     a.zp[i] = (uint32_t*)zptrs[i];
-    a.zstart[i + 1] = a.zstart[i] + (long)(zbytes[i] / 4);
+    a.zvec = a.zvec && zbytes[i] % 16 == 0 && ((uintptr_t)zptrs[i] & 15) == 0;
   }
+  for (int i = 0; i < zcount; ++i) a.zstart[i + 1] = a.zstart[i] + (long)(zbytes[i] / (a.zvec ? 16 : 4));
   long mx = 0;
   for (int i = 0; i < n; ++i) {
     const cv_conv_pack& p = items[i];
@@ -1503,8 +1507,9 @@ static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, con
     gx = t > gx ? t : gx;
   }
   if (!tiled) gx = (mx + 255) / 256;
-  if (zcount) {
-    const long zg = (a.zstart[zcount] + 255) / 256;
+  if (zcount) {  // (the zero slice walks its buffers grid-stride, ~4 units per thread: it widens the grid only as far
+                 // as that needs, so the small layers' rows of the grid are not mostly empty workgroups)
+    const long zg = (a.zstart[zcount] + 1023) / 1024;
     gx = zg > gx ? zg : gx;
   }
   if (gx > 1024) gx = 1024;
