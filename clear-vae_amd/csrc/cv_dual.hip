@@ -28,6 +28,17 @@ thread_local DirectCap* g_direct_cap = nullptr;
 namespace dual {
 
 constexpr long kMaxDirect = 512;  // direct workgroups of a served dual grid (one resident round)
+// CV_DUAL_MAXD (A/B): a larger cap (VAE64's 1024-workgroup conv2 pair measured slower as a dual grid in round 4,
+// with the roles alternating)
+static long max_direct() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_DUAL_MAXD");
+    v = e ? atol(e) : kMaxDirect;
+    if (v < 1) v = kMaxDirect;
+  }
+  return v;
+}
 
 struct DualMap {
   int nd, dgx, dgy;       // direct workgroups and their grid
@@ -76,6 +87,9 @@ static const Ent k_pairs[] = {
     CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 32, 2, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
     CV_DUAL(OP_GATHER, CV_XF_BNBWD, CV_STAT_BWD, 64, 4, 64, 64, CV_XF_BNRELU, CV_XF_BNBWD, CV_STAT_NONE, 2, 0),
     CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 64, 1, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
+    // VAE64's conv3 pair (bs = 256) and PACS's conv2 pair (bs = 32)
+    CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 64, 2, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
+    CV_DUAL(OP_SCATTER, CV_XF_BNBWD, CV_STAT_BWD, 32, 1, 64, 64, CV_XF_BNBWD, CV_XF_BNRELU, CV_STAT_NONE, 2, 0),
 };
 #undef CV_DUAL
 
@@ -121,7 +135,7 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
     const long nd = (long)d.grid.x * d.grid.y, ng = (long)g.grid.x * g.grid.y * g.grid.z;
     // (a direct grid of more than one resident round — VAE64's conv2 at 256 images, 1024 workgroups — measured
     // slower as a dual grid, 174 -> 215 us; MNIST's pairs at 512 direct workgroups gain 4-5 us each)
-    if (fn && nd <= kMaxDirect && nd + ng < (1L << 31)) {
+    if (fn && nd <= max_direct() && nd + ng < (1L << 31)) {
       const size_t lds = d.lds > g.lds ? d.lds : g.lds;
       bool ok = true;
       if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -164,6 +178,14 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
       }
     }
   }
+  {
+    static int log = -1;
+    if (log < 0) log = getenv("CV_DUAL_LOG") ? 1 : 0;
+    if (log && d.got && g.got)
+      fprintf(stderr, "dual-unserved dkey=%d,%d,%d,%d,%d gkey=%d,%d,%d,%d,%d,%d,%d nd=%ld ng=%ld\n", d.key[0], d.key[1],
+              d.key[2], d.key[3], d.key[4], g.key[0], g.key[1], g.key[2], g.key[3], g.key[4], g.key[5], g.key[6],
+              (long)d.grid.x * d.grid.y, (long)g.grid.x * g.grid.y * g.grid.z);
+  }
   int r = 0;
   if (d.got) {
     d.got = false;
@@ -182,7 +204,7 @@ static thread_local fast::GemmCap t_gcap;
 
 int dual_wgrad_bm_cap() {  // (only when the captured direct launch belongs to a served pair)
   if (!direct::g_direct_cap || !t_dcap.got || !dual::enabled()) return 0;
-  return ((long)t_dcap.grid.x * t_dcap.grid.y <= dual::kMaxDirect && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
+  return ((long)t_dcap.grid.x * t_dcap.grid.y <= dual::max_direct() && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
 }
 
 // Workgroup slots the weight-gradient role of a served dual grid has in the grid's first resident round (0: no
