@@ -730,6 +730,8 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
+            from cvhip.dist import prepare_captured_collectives_env
+            prepare_captured_collectives_env()
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)

@@ -17,8 +17,21 @@ runs on CPU tensors with the gloo backend in the tests.
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+
+def prepare_captured_collectives_env() -> None:
+    """Call before creating an RCCL process group whose collectives a step graph will capture
+    (CVHIP_GRAPH_COLLECTIVES=1).  A collective captured into the graph records its completion event inside
+    the capture; with the process group's event cache on (its default) that event object is handed back to
+    the cache and reused by a later eager collective, and the group's watchdog thread then fails querying it
+    ("operation not permitted on an event last recorded in a capturing stream", seen intermittently in
+    tests/test_gpu_graph_collectives.py).  Fresh events per collective remove the reuse."""
+    if os.environ.get("CVHIP_GRAPH_COLLECTIVES", "0") == "1":
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 def world() -> int:

@@ -24,6 +24,8 @@ def main(mode, steps, port, n=64, timed=0):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     torch.manual_seed(1234)  # (the engine's Philox stream is keyed by torch's seed: both runs draw the same noise)
+    from cvhip.dist import prepare_captured_collectives_env
+    prepare_captured_collectives_env()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from cvhip.engine import ClearStep
     from oracle import cpu_ref as R
