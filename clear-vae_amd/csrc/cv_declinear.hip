@@ -261,6 +261,8 @@ struct BwdArgs {
   const float* w;       // [F][K] the Linear's weight (dz != nullptr)
   float* dz;            // [n][K] += d(h) W over the workgroup's 16 features (fp32 atomics; caller zeroes), or nullptr
   int n, K, F, pix, ch;
+  int hold;  // keep pass 1's single load batch in registers for pass 2 (CV_DL_HOLD, A/B; default 1)
+  int rot;   // rotate the row tiles' order by workgroup (CV_DL_ROT, A/B; default 1)
 };
 
 constexpr int TB = 4;  // 16-row tiles whose elementwise loads are in flight together (per wave)
@@ -290,27 +292,34 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   __syncthreads();
   const BnFwdC k = kf[lr];
   // this lane's elements: rows 16 tile + 4 lq + r of column col, tiles w, w + 4, ...
+  // Row-tile order rotated by workgroup: every workgroup adds its dz partials onto the same [n][K] rows, so in a
+  // common order all of them hit one 16-row block at a time; the wave offset and the slot rotation spread them over
+  // NW TB blocks.  Register slot i holds tile tile0 + NW ((i + sr) % TB): static slots, rotated tiles.
+  const int wr = A.rot ? (w + (int)blockIdx.x) % NW : w, sr = A.rot ? ((int)blockIdx.x / NW) & (TB - 1) : 0;
+  auto tile_at = [&](int tile0, int i) { return tile0 + NW * ((i + sr) & (TB - 1)); };
   auto load = [&](int tile0, float (*hv)[4], float (*dv)[4]) {
 #pragma unroll
     for (int i = 0; i < TB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * (tile0 + NW * i) + 4 * lq + r;
+        const int row = 16 * tile_at(tile0, i) + 4 * lq + r;
         const size_t o = (size_t)(row < n ? row : 0) * F + col;
         hv[i][r] = A.h[o];
         dv[i][r] = A.ga[o];
       }
   };
-  // ---- pass 1: ReLU mask, backward sums
+  // ---- pass 1: ReLU mask, backward sums.  When every wave's rows fit one load batch (nt <= NW TB: MNIST / VAE64
+  // at n <= 512), the batch stays in registers for pass 2 instead of being loaded again.
   double s1 = 0.0, s2 = 0.0;
-  for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
-    float hv[TB][4], dv[TB][4];
+  const bool held = A.hold && nt <= NW * TB;
+  float hv[TB][4], dv[TB][4];
+  for (int tile0 = wr; tile0 < nt; tile0 += NW * TB) {
     load(tile0, hv, dv);
 #pragma unroll
     for (int i = 0; i < TB; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 16 * (tile0 + NW * i) + 4 * lq + r;
+        const int row = 16 * tile_at(tile0, i) + 4 * lq + r;
         if (row >= n) continue;
         const float dm = bn_out(hv[i][r], k) <= 0.f ? 0.f : dv[i][r];
         s1 += (double)dm;
@@ -357,13 +366,12 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
         wz[jt][s] = j < K ? A.w[(size_t)fc * K + j] : 0.f;
       }
   }
-  for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
-    float hv[TB][4], dv[TB][4];
-    load(tile0, hv, dv);
+  for (int tile0 = wr; tile0 < nt; tile0 += NW * TB) {
+    if (!held) load(tile0, hv, dv);
 #pragma unroll
     for (int i = 0; i < TB; ++i) {
-      const int tile = tile0 + NW * i;
-      if (tile >= nt) break;
+      const int tile = tile_at(tile0, i);
+      if (tile >= nt) continue;
       f32x4 dp;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -841,6 +849,26 @@ extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const fl
   a.gw = gweight;
   a.w = weight;
   a.dz = dz;
+  {
+    static int abl = -1;  // CV_DL_ABLATE=1: timing probe only (wrong dz): drop the dz partial atomics
+    if (abl < 0) {
+      const char* e = getenv("CV_DL_ABLATE");
+      abl = e ? atoi(e) : 0;
+    }
+    if (abl & 1) a.dz = nullptr;
+    static int hold = -1;
+    if (hold < 0) {
+      const char* e = getenv("CV_DL_HOLD");
+      hold = e ? atoi(e) : 1;
+    }
+    a.hold = hold;
+    static int rot = -1;
+    if (rot < 0) {
+      const char* e = getenv("CV_DL_ROT");
+      rot = e ? atoi(e) : 1;
+    }
+    a.rot = rot;
+  }
   a.n = g->n;
   a.K = K;
   a.F = F;
