@@ -39,6 +39,17 @@ constexpr int DF = 16;          // storage columns per workgroup
 constexpr int NW = NTD / 64;    // waves
 constexpr int ZMAX = 16384;     // latents staged in LDS (n * KR)
 
+// CV_DL_PRE (A/B; default 1): the backward kernels issue their first batch of activation loads before staging the
+// small operand (z / dheads) in LDS, so the cold activation reads' latency runs under the staging
+static int dl_pre() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_DL_PRE");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
 __device__ __forceinline__ int feature_of(int col, int pix, int ch) {  // PyTorch feature c*pix + p
   if (pix <= 1) return col;
   const int p = col / ch;
@@ -263,6 +274,7 @@ struct BwdArgs {
   int n, K, F, pix, ch;
   int hold;  // keep pass 1's single load batch in registers for pass 2 (CV_DL_HOLD, A/B; default 1)
   int rot;   // rotate the row tiles' order by workgroup (CV_DL_ROT, A/B; default 1)
+  int pre;   // dl_pre()
 };
 
 constexpr int TB = 4;  // 16-row tiles whose elementwise loads are in flight together (per wave)
@@ -280,18 +292,6 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   __shared__ BnBwdC kb[DF];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
   const int col0 = blockIdx.x * DF, col = col0 + lr;
-  stage_pad<KR>(A.z, n, K, sz);
-  if (t < DF) {  // forward constants of the workgroup's features (replica fold, one thread per feature)
-    const int fc = feature_of(col0 + t, A.pix, A.ch);
-    double s, q;
-    bn_sums(A.bn.stat, F, fc, s, q);
-    fs[0][t] = s;
-    fs[1][t] = q;
-    kf[t] = bn_fwd_const_s(A.bn, fc, s, q);
-  }
-  __syncthreads();
-  const BnFwdC k = kf[lr];
-  // this lane's elements: rows 16 tile + 4 lq + r of column col, tiles w, w + 4, ...
   // Row-tile order rotated by workgroup: every workgroup adds its dz partials onto the same [n][K] rows, so in a
   // common order all of them hit one 16-row block at a time; the wave offset and the slot rotation spread them over
   // NW TB blocks.  Register slot i holds tile tile0 + NW ((i + sr) % TB): static slots, rotated tiles.
@@ -308,13 +308,26 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
         dv[i][r] = A.ga[o];
       }
   };
+  float hv[TB][4], dv[TB][4];
+  if (A.pre && wr < nt) load(wr, hv, dv);  // (in flight under the staging)
+  stage_pad<KR>(A.z, n, K, sz);
+  if (t < DF) {  // forward constants of the workgroup's features (replica fold, one thread per feature)
+    const int fc = feature_of(col0 + t, A.pix, A.ch);
+    double s, q;
+    bn_sums(A.bn.stat, F, fc, s, q);
+    fs[0][t] = s;
+    fs[1][t] = q;
+    kf[t] = bn_fwd_const_s(A.bn, fc, s, q);
+  }
+  __syncthreads();
+  const BnFwdC k = kf[lr];
+  // this lane's elements: rows 16 tile + 4 lq + r of column col, tiles w, w + 4, ...
   // ---- pass 1: ReLU mask, backward sums.  When every wave's rows fit one load batch (nt <= NW TB: MNIST / VAE64
   // at n <= 512), the batch stays in registers for pass 2 instead of being loaded again.
   double s1 = 0.0, s2 = 0.0;
   const bool held = A.hold && nt <= NW * TB;
-  float hv[TB][4], dv[TB][4];
   for (int tile0 = wr; tile0 < nt; tile0 += NW * TB) {
-    load(tile0, hv, dv);
+    if (!(A.pre && tile0 == wr)) load(tile0, hv, dv);
 #pragma unroll
     for (int i = 0; i < TB; ++i)
 #pragma unroll
@@ -431,6 +444,7 @@ struct HeadsArgs {
   float* gb;            // [J] += (workgroup 0)
   int n, J, F, pix, ch;
   cv_latent_chain chain;  // chain.dz != nullptr: the decoder chain term is added to dheads while staging it
+  int pre;                // dl_pre()
 };
 
 // stage_pad of dheads [n][J = 4d] with the decoder chain term of cv_latent_combine added (cv_latent_chain): column
@@ -484,6 +498,17 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
   const int col0 = blockIdx.x * DF, col = col0 + lr;
   const int f = feature_of(col, A.pix, C);
+  float yv[TB][4];
+  auto loady = [&](int tile0) {
+#pragma unroll
+    for (int i = 0; i < TB; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbeg + 16 * (tile0 + NW * i) + 4 * lq + r;
+        yv[i][r] = A.y[(size_t)(row < n ? row : 0) * F + col];
+      }
+  };
+  if (A.pre && w < nt) loady(w);  // (in flight under the staging)
   f32x4 b[JR / 16];  // B fragments: W[j][f], j = 16 c + 4 lq + s
 #pragma unroll
   for (int c = 0; c < JR / 16; ++c)
@@ -517,14 +542,7 @@ __global__ __launch_bounds__(NTD) void heads_bwd_kernel(const HeadsArgs A) {
   for (int j = 0; j < JR / 16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   double s1 = 0.0, s2 = 0.0;
   for (int tile0 = w; tile0 < nt; tile0 += NW * TB) {
-    float yv[TB][4];
-#pragma unroll
-    for (int i = 0; i < TB; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbeg + 16 * (tile0 + NW * i) + 4 * lq + r;
-        yv[i][r] = A.y[(size_t)(row < n ? row : 0) * F + col];
-      }
+    if (!(A.pre && tile0 == w)) loady(tile0);
 #pragma unroll
     for (int i = 0; i < TB; ++i) {
       const int tile = tile0 + NW * i;
@@ -868,6 +886,7 @@ extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const fl
       rot = e ? atoi(e) : 1;
     }
     a.rot = rot;
+    a.pre = dl_pre();
   }
   a.n = g->n;
   a.K = K;
@@ -948,6 +967,7 @@ static int heads_backward(const cv_linear* g, const float* dheads, const cv_late
   a.ch = ch;
   memset(&a.chain, 0, sizeof(a.chain));
   if (chain) a.chain = *chain;
+  a.pre = dl_pre();
   // row splits (CV_HEADS_RS, A/B; default 1): the 128 feature workgroups leave half the CUs idle, but splitting
   // their rows measured slower — MNIST 0.4948 -> 0.4980 ms (2 splits) / 0.5056 (4), CelebA neutral / +0.7 % time —
   // the per-workgroup prologue (B fragments, the finalised constants) and the atomics outweigh the shorter tile loop.
