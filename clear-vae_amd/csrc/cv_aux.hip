@@ -91,7 +91,7 @@ void aux_count_merged() { ++aux::g_merged; }
 // the caller launches the direct kernel alone and the phase stays queued)
 int direct_aux_launch(const int* dkey, const direct::DArgs& da, dim3 dgrid, size_t dlds, hipStream_t st) {
   using namespace aux;
-  if (!g_aux.set || !enabled()) return -1;
+  if (!g_aux.set || !enabled() || g_aux.stream != st) return -1;  // (queued for another stream: not this launch's)
   const NtArgs& pa = g_aux.a;
   if ((pa.with_combine && g_aux.phase != 0) || pa.d > 8 || pa.n > NT_MAXN) return -1;
   const int dm = 8;

@@ -965,7 +965,8 @@ extern "C" int cv_output_loss(const cv_bn* bn, const float* y, const float* x, i
   const OutLossArgs A{*bn, y, x, n, c, hw, FDiv::make(c), FDiv::make(hw), xhat, rec_out, dv_out, gstat_out, rec_scale};
   // a queued NT-Xent gradient phase rides in this grid where served (cv_ntxent_aux; else it stays queued for its
   // flush)
-  if (g_aux.set && g_aux.phase == 1 && aux_enabled() && g_aux.a.d <= 8 && !g_aux.a.with_combine &&
+  if (g_aux.set && g_aux.stream == S(stream) && g_aux.phase == 1 && aux_enabled() && g_aux.a.d <= 8 &&
+      !g_aux.a.with_combine &&
       ntxent_reg_ok(g_aux.a, g_aux.a.nbr)) {
     const NtArgs P = g_aux.a;
     const int agx = (P.n + P.rpb - 1) / P.rpb;

@@ -122,30 +122,44 @@ __global__ __launch_bounds__(1024) void combine_kernel(const CombineArgs C) {
 }
 
 // The combine over several workgroups (one batch of 8 elements per thread each): the element-wise d(heads) terms
-// are the one-workgroup kernel's, the KL sums meet in two fp64 accumulators (device atomics, then an arrival count);
-// the last workgroup to arrive writes the losses and resets the accumulators and the count for the next launch.
-// A single workgroup walking n x 2d elements in 8-element batches was a chain of dependent round trips on the
-// step's critical path (MNIST 10 us, VAE64 17 us).  CV_COMBINE_WG=0: the one-workgroup kernel (A/B).
-__device__ double g_comb_acc[2];
-__device__ unsigned g_comb_ticket;
+// are the one-workgroup kernel's; each workgroup writes its two fp64 KL partials into its own slot of the caller's
+// workspace, releases them (agent-scope fence) and takes the arrival ticket; the last workgroup to arrive acquires,
+// sums the slots in workgroup order (the result does not depend on the arrival order: bit-reproducible run to run),
+// writes the losses and resets the ticket for the next launch.  Nothing is shared between launches that do not share
+// a workspace (two steps on two streams each own one).  A single workgroup walking n x 2d elements in 8-element
+// batches was a chain of dependent round trips on the step's critical path (MNIST 10 us, VAE64 17 us).
+// CV_COMBINE_WG=0, or no workspace: the one-workgroup kernel.
 constexpr int CMB_NT = 256;
-__global__ __launch_bounds__(CMB_NT) void combine_multi_kernel(const CombineArgs C) {
+constexpr int CMB_MAXG = 64;
+__global__ __launch_bounds__(CMB_NT) void combine_multi_kernel(const CombineArgs C, double* __restrict__ work) {
   __shared__ double scratch[16];
   __shared__ int last;
   double kc, ks;
   const float w = combine_sums<CMB_NT>(C, blockIdx.x * CMB_NT * 8, gridDim.x * CMB_NT * 8, scratch, &kc, &ks);
+  unsigned* ticket = reinterpret_cast<unsigned*>(work + 2 * CMB_MAXG);
   if (threadIdx.x == 0) {
-    atomic_add_f64(g_comb_acc, kc);
-    atomic_add_f64(g_comb_acc + 1, ks);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(&g_comb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const double a = __hip_atomic_load(g_comb_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const double b = __hip_atomic_load(g_comb_acc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g_comb_acc, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g_comb_acc + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&g_comb_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    work[2 * blockIdx.x] = kc;
+    work[2 * blockIdx.x + 1] = ks;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x < 64) {  // (one wave: the partials in workgroup order, a fixed-shape fp64 tree)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int t = threadIdx.x;
+    double a = 0.0, b = 0.0;
+    if (t < (int)gridDim.x) {
+      a = __hip_atomic_load(work + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      b = __hip_atomic_load(work + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o, 64);
+      b += __shfl_down(b, o, 64);
+    }
+    if (t == 0) {
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (C.rec_in) {
         double r = 0.0;
         for (int q = 0; q < CV_REC_REPL; ++q) r += C.rec_in[q];
@@ -158,7 +172,7 @@ __global__ __launch_bounds__(CMB_NT) void combine_multi_kernel(const CombineArgs
   }
 }
 
-static void combine_launch(const CombineArgs& C, hipStream_t st) {
+static void combine_launch(const CombineArgs& C, double* work, hipStream_t st) {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("CV_COMBINE_WG");
@@ -166,13 +180,13 @@ static void combine_launch(const CombineArgs& C, hipStream_t st) {
   }
   const long total = (long)C.n * 2 * C.d;
   long g = (total + CMB_NT * 8 - 1) / (CMB_NT * 8);
-  if (g > 64) g = 64;
-  if (!mode || g < 2) {
+  if (g > CMB_MAXG) g = CMB_MAXG;
+  if (!mode || g < 2 || !work) {
     hipLaunchKernelGGL(combine_kernel, dim3(1), dim3(1024), 0, st, C);
     return;
   }
   note_launch((const void*)combine_multi_kernel);
-  hipLaunchKernelGGL(combine_multi_kernel, dim3((unsigned)g), dim3(CMB_NT), 0, st, C);
+  hipLaunchKernelGGL(combine_multi_kernel, dim3((unsigned)g), dim3(CMB_NT), 0, st, C, work);
 }
 
 // ---------------------------------------------------------------- reconstruction MSE (autograd path)
@@ -747,24 +761,26 @@ extern "C" int cv_kl(const float* mu, const float* logvar, int ld, int n, int d,
   return 0;
 }
 
+extern "C" size_t cv_latent_combine_workspace_bytes(void) { return (2 * CMB_MAXG + 1) * sizeof(double); }
+
 extern "C" int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                                  float loc, float scale, const int64_t* anneal_step, const double* rec_in,
-                                 float* dheads, float* losses, cv_stream_t stream) {
+                                 float* dheads, float* losses, double* work, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine: bad args");
   const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 0};
-  combine_launch(C, S(stream));
+  combine_launch(C, work, S(stream));
   CV_LAUNCH_CHECK("latent_combine");
   return 0;
 }
 
 extern "C" int cv_latent_combine_acc(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                                      float loc, float scale, const int64_t* anneal_step, const double* rec_in,
-                                     float* dheads, float* losses, cv_stream_t stream) {
+                                     float* dheads, float* losses, double* work, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(heads && z && anneal_step && dheads && losses && n > 0 && d > 0, "latent_combine_acc: bad args");
   const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 1};
-  combine_launch(C, S(stream));
+  combine_launch(C, work, S(stream));
   CV_LAUNCH_CHECK("latent_combine_acc");
   return 0;
 }
@@ -843,12 +859,13 @@ extern "C" int cv_ntxent_aux(const cv_ntxent_branch* br, int nbr, const int64_t*
   if (ntxent_args(br, nbr, label, n, d, sim, temperature, accumulate, a)) return 1;
   a.nbr = nbr;
   a.rpb = ntxent_reg_ok(a, nbr) ? ntr_rows() : NTL_ROWS;
-  if (g_aux.set) {  // a phase no launch took (its flush was skipped): it runs now, in queue order
+  if (g_aux.set) {  // a phase no launch took (its flush was skipped): it runs now, on the stream it was queued for
     g_aux.set = 0;
-    if (ntxent_launch(g_aux.a, g_aux.a.nbr, g_aux.phase == 0, S(stream))) return 2;
+    if (ntxent_launch(g_aux.a, g_aux.a.nbr, g_aux.phase == 0, g_aux.stream)) return 2;
   }
   g_aux.a = a;
   g_aux.phase = phase;
+  g_aux.stream = S(stream);
   g_aux.set = 1;
   return 0;
 }
@@ -868,10 +885,20 @@ extern "C" int cv_ntxent_aux_combine(const float* heads, const float* z, int n, 
 
 extern "C" int cv_ntxent_aux_flush(cv_stream_t stream) {
   clear_error();
+  (void)stream;
   if (!g_aux.set) return 0;
   g_aux.set = 0;
-  return ntxent_launch(g_aux.a, g_aux.a.nbr, g_aux.phase == 0, S(stream)) ? 2 : 0;
+  // (on the stream the phase was queued for: a flush issued on another stream must not move it there)
+  return ntxent_launch(g_aux.a, g_aux.a.nbr, g_aux.phase == 0, g_aux.stream) ? 2 : 0;
 }
+
+extern "C" int cv_ntxent_aux_discard(void) {
+  const int had = g_aux.set;
+  g_aux.set = 0;
+  return had;
+}
+
+extern "C" int cv_ntxent_aux_pending(void) { return g_aux.set ? 1 + g_aux.phase : 0; }
 
 extern "C" int cv_latent_step(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                               float loc, float scale, const int64_t* anneal_step, const double* rec_in,

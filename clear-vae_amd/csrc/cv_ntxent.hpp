@@ -788,9 +788,13 @@ __device__ __forceinline__ void ntxent_grad_reg_body(const NtArgs& A, const int 
 }
 
 // An NT-Xent phase (0: row log-sum-exps, 1: losses + gradients) queued by cv_ntxent_aux to run as extra workgroups
-// of this thread's next direct-kernel launch (cv_aux.hip); cv_ntxent_aux_flush launches it alone if none took it.
+// of this thread's next direct-kernel launch ON THE STREAM IT WAS QUEUED FOR (cv_aux.hip, cv_output_loss; a launch
+// on another stream leaves it queued); cv_ntxent_aux_flush launches it alone, on that stream, if none took it, and
+// cv_ntxent_aux_discard drops it (the engine's error path: a program that raised between the queue and its flush
+// must not leave a request whose pointers belong to that step).
 struct AuxPend {
   int set, phase;
+  hipStream_t stream;
   NtArgs a;
 };
 extern thread_local AuxPend g_aux;

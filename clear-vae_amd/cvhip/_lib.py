@@ -274,13 +274,16 @@ _SIGS = {
     "cv_latent_combine": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
-         c_void_p, c_void_p],
+         c_void_p, c_void_p, c_void_p],
     ),
     "cv_ntxent_aux": (
         c_int,
         [_P(cv_ntxent_branch), c_int, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p],
     ),
     "cv_ntxent_aux_flush": (c_int, [c_void_p]),
+    "cv_ntxent_aux_discard": (c_int, []),
+    "cv_latent_combine_workspace_bytes": (c_size_t, []),
+    "cv_ntxent_aux_pending": (c_int, []),
     "cv_ntxent_aux_combine": (
         c_int,
         [c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -288,7 +291,7 @@ _SIGS = {
     "cv_latent_combine_acc": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p,
-         c_void_p, c_void_p],
+         c_void_p, c_void_p, c_void_p],
     ),
     "cv_mse_sum": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cv_ntxent": (

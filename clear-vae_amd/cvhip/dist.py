@@ -34,6 +34,40 @@ def prepare_captured_collectives_env() -> None:
         os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
+_CAPTURE_GROUP = None
+
+
+def captured_collectives_group():
+    """The process group a step graph captures its all-reduces on (CVHIP_GRAPH_COLLECTIVES=1).
+
+    A dedicated RCCL group over every rank, constructed with its CUDA-event cache off
+    (TORCH_NCCL_CUDA_EVENT_CACHE=0 while the group is built: ProcessGroupNCCL reads it in its constructor).
+    With the cache on, a completion event recorded inside the capture goes back to the cache and is reused by a
+    later eager collective, which the group's watchdog then fails to query ("operation not permitted on an event
+    last recorded in a capturing stream", hipErrorCapturedEvent, an abort of the process).  The step's bucket
+    collectives, eager first step included, run only on this group, so the default group's setting (whoever
+    created it, whenever) cannot reach that abort.  Collective: every rank must call it, in the same order."""
+    global _CAPTURE_GROUP
+    if not (dist.is_available() and dist.is_initialized()):
+        raise RuntimeError("captured collectives need an initialised torch.distributed process group")
+    if dist.get_backend() != "nccl":
+        raise RuntimeError("captured collectives need the nccl (RCCL) backend: a %r collective cannot be captured "
+                           "into a HIP graph (unset CVHIP_GRAPH_COLLECTIVES)" % dist.get_backend())
+    world_pg = dist.group.WORLD
+    if _CAPTURE_GROUP is None or _CAPTURE_GROUP[0] is not world_pg:  # (none yet, or the default group was rebuilt)
+        key = "TORCH_NCCL_CUDA_EVENT_CACHE"
+        prev = os.environ.get(key)
+        os.environ[key] = "0"
+        try:
+            _CAPTURE_GROUP = (world_pg, dist.new_group(backend="nccl"))
+        finally:
+            if prev is None:
+                del os.environ[key]
+            else:
+                os.environ[key] = prev
+    return _CAPTURE_GROUP[1]
+
+
 def world() -> int:
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size()

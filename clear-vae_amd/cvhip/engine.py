@@ -58,7 +58,9 @@ FUSED_ADAM = os.environ.get("CVHIP_FUSED_ADAM", "0") == "1"  # measured slower (
 # collective's branch runs beside the next backward segment and the Adam segment waits on it), so a step is one
 # graph launch from the host instead of 4 launches + 3 all-reduce calls + 1 wait (CLEAR-MIM: + 5 x (launch,
 # all-reduce, wait, launch)).  Off by default: it needs a backend that supports stream capture (RCCL; not gloo,
-# which the world-2 tests use), and the one-GPU box can only rehearse it at world 1 (tests/test_gpu_graph_collectives.py).
+# which the world-2 tests use: ClearStep refuses it), and the one-GPU box can only rehearse it at world 1
+# (tests/test_gpu_graph_collectives.py).  The bucket collectives then run on a dedicated RCCL group created with
+# its CUDA-event cache off (cvhip.dist.captured_collectives_group), so no caller setup is needed.
 GRAPH_COLLECTIVES = os.environ.get("CVHIP_GRAPH_COLLECTIVES", "0") == "1"
 
 # CVHIP_LATENT_SIDE=1 (A/B knob, off: measured slower): the NT-Xent terms depend only on the heads, so their two launches (row
@@ -268,9 +270,14 @@ class ClearStep:
             cvdist.broadcast_flat(self.arena.flat)
             if self.two_nets:
                 cvdist.broadcast_flat(self.est_arena.flat)
-            self.buckets = cvdist.GradBuckets(self.arena.grad, self.bucket_bounds(), force=True)
+            # captured collectives run on their own RCCL group built with the event cache off
+            # (cvdist.captured_collectives_group: the abort a cached captured event causes cannot be reached,
+            # whatever the default group's settings; a non-RCCL backend is refused here, before any capture)
+            cgroup = cvdist.captured_collectives_group() if self.capture_collectives else None
+            self.buckets = cvdist.GradBuckets(self.arena.grad, self.bucket_bounds(), group=cgroup, force=True)
             if self.two_nets:
-                self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)], force=True)
+                self.est_buckets = cvdist.GradBuckets(self.est_arena.grad, [(0, self.est_arena.numel)], group=cgroup,
+                                                      force=True)
         # grads visible through p.grad (like the reference after loss.backward())
         for p in self.arena.params:
             p.grad = self.arena.gview(p)
@@ -445,7 +452,7 @@ class ClearStep:
                 lat.add_join()
             lat.add("cv_latent_combine_acc", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
                     ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
-                    ws.rec, ws.dheads, ws.losses)
+                    ws.rec, ws.dheads, ws.losses, ws.comb_work)
             lat_inj = Program()
             lat_inj.extend(lat)
         if branches is not None and not side_nt and not aux_nt:

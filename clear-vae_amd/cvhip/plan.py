@@ -473,6 +473,15 @@ class Program:
         run joins it: the side stream is one ordered queue); graph capture needs a join before its end.
         timer (eager measurement only, bench.py): a list that receives (call index, start, end) timing
         events recorded around each call on the stream the call runs on."""
+        try:
+            self._run(stream, join, timer)
+        except BaseException:
+            # a queued NT-Xent phase (cv_ntxent_aux) whose flush this program did not reach holds this step's
+            # pointers: drop it, so the next queue or served launch does not issue it
+            _lib.lib().cv_ntxent_aux_discard()
+            raise
+
+    def _run(self, stream, join, timer):
         s = _lib.stream_handle() if stream is None else stream
         main = torch.cuda.current_stream()
         if not any(c[3] for c in self.calls):
@@ -620,6 +629,9 @@ class Workspace:
             self.g_dec = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.dec]
             self.lse = torch.empty(2, 2 * n, **f32)  # contrastive row log-sum-exps (2 branches)
             self.losses = torch.zeros(8, **f32)
+            # the multi-workgroup latent combine's KL partial slots + arrival ticket (zeroed once; left zeroed)
+            self.comb_work = torch.zeros(int(_lib.lib().cv_latent_combine_workspace_bytes()) // 8 + 1,
+                                         dtype=torch.float64, device=f32["device"])
             self.mi_work = torch.zeros(int(_lib.lib().cv_mi_workspace_bytes(n)) // 4 + 16, **f32)
             # split-K partial tiles of the weight-gradient GEMMs (one launch at a time on the stream)
             L = _lib.lib()

@@ -355,15 +355,20 @@ int cv_kl(const float* mu, const float* logvar, int ld, int n, int d, float* kl_
  * losses[1], losses[2] = kl_c, kl_s; losses[7] = w.  dheads is overwritten. */
 int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                       float loc, float scale, const int64_t* anneal_step, const double* rec_in,
-                      float* dheads, float* losses, cv_stream_t stream);
+                      float* dheads, float* losses, double* work, cv_stream_t stream);
 /* cv_latent_combine with dheads += instead of overwritten: the fused step whose NT-Xent gradients were already
- * accumulated into a zeroed dheads (their launches run on a side stream during the decoder pass, and the step
- * joins it before this call; cvhip/engine.py LATENT_SIDE). */
+ * accumulated into a zeroed dheads — the default schedule (cvhip/engine.py LATENT_AUX: the NT-Xent phases ride in the
+ * decoder's ConvTranspose2d forward grids and this call follows the decoder backward), or the opt-in side stream
+ * (LATENT_SIDE, joined before this call). */
 int cv_latent_combine_acc(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                           float loc, float scale, const int64_t* anneal_step, const double* rec_in,
-                          float* dheads, float* losses, cv_stream_t stream);
-/* (Both combine entries run over several workgroups when n x 2d >= 4096 elements, their KL sums meeting in a
- * per-device accumulator: two combine launches on one device must not overlap in time — e.g. on two streams.) */
+                          float* dheads, float* losses, double* work, cv_stream_t stream);
+/* work (or NULL): a caller-owned device workspace of cv_latent_combine_workspace_bytes(), zeroed once before its
+ * first use (it is left zeroed after every call).  With it, batches of n x 2d >= 4096 elements run over several
+ * workgroups whose KL partials are summed in workgroup order by the last to arrive (bit-reproducible, independent of
+ * arrival order); NULL runs the one-workgroup kernel.  Two launches that may overlap in time (two streams) need two
+ * workspaces. */
+size_t cv_latent_combine_workspace_bytes(void);
 
 /* reconstruction term (losses.py:45-47) for the autograd path: rec = mean_n sum (xhat - x)^2;
  * work: one zeroed fp64 word.  dxhat != NULL: dxhat = gscale[0] * 2 (xhat - x) / n. */
@@ -387,14 +392,19 @@ int cv_ntxent(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, 
               float temperature, int phase, int accumulate, cv_stream_t stream);
 /* An NT-Xent phase of cv_ntxent (phase 0: the row log-sum-exps; 1: the losses and gradients, accumulated into the
  * branches' d(mu) / d(logvar) when accumulate) queued to run as extra workgroups of this thread's next direct-kernel
- * conv launch on `stream`'s order (cv_aux.hip: MNIST's decoder ConvTranspose2d forwards serve it); the call after
- * that conv must be cv_ntxent_aux_flush, which launches the phase on its own if no launch took it.  One phase at
- * a time (a phase still queued when the next is queued is launched first, on `stream`); the phases read only the
- * heads and labels (trainer.py:474-479, losses.py:98-137), so the fused step
- * queues them into its decoder forward.  The branch gradients must not be read before the flush. */
+ * conv launch on the SAME `stream` (cv_aux.hip: MNIST's decoder ConvTranspose2d forwards serve it; a launch on another
+ * stream leaves it queued); the call after that conv must be cv_ntxent_aux_flush, which launches the phase on its own,
+ * on the stream it was queued for, if no launch took it.  One phase at a time (a phase still queued when the next is
+ * queued is launched first, on its own stream); the phases read only the heads and labels (trainer.py:474-479,
+ * losses.py:98-137), so the fused step queues them into its decoder forward.  The branch gradients must not be read
+ * before the flush.  cv_ntxent_aux_discard drops a queued phase without launching it (returns 1 if one was queued):
+ * the engine calls it when a program raises between the queue and its flush.  cv_ntxent_aux_pending: 0, or 1 + the
+ * queued phase (test hook). */
 int cv_ntxent_aux(const cv_ntxent_branch* br, int nbr, const int64_t* label, int n, int d, int sim, float temperature,
                   int phase, int accumulate, cv_stream_t stream);
 int cv_ntxent_aux_flush(cv_stream_t stream);
+int cv_ntxent_aux_discard(void);
+int cv_ntxent_aux_pending(void);
 /* Attach the KL part of the latent combine (cv_latent_combine with dz = NULL and rec_in = NULL: losses[1], [2], [7]
  * and dheads = the KL gradient, overwritten — dheads must not hold anything yet) to the queued phase-0 request, as
  * one more workgroup of the same grid (or of the flush launch).  The decoder chain term follows in

@@ -24,8 +24,8 @@ def main(mode, steps, port, n=64, timed=0):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     torch.manual_seed(1234)  # (the engine's Philox stream is keyed by torch's seed: both runs draw the same noise)
-    from cvhip.dist import prepare_captured_collectives_env
-    prepare_captured_collectives_env()
+    # (no caller setup for the captured form: the default group is built with whatever event-cache setting the
+    # environment holds — the test sets the cache ON — and the engine captures on its own group)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from cvhip.engine import ClearStep
     from oracle import cpu_ref as R
@@ -79,6 +79,7 @@ def main(mode, steps, port, n=64, timed=0):
     flat = eng.arena.flat.cpu().numpy()
     print(json.dumps({"mode": mode, "n": n, "ms_per_step": ms, "losses": losses, "digest": digest, "one_graph": bool(G.get("one_graph")),
                       "ngraphs": len(G.get("graphs", [])), "capture": eng.capture_collectives,
+                      "own_group": eng.buckets.group is not None,
                       "flat_head": [float(v) for v in flat[:8]], "flat_hash": float(np.abs(flat).astype(np.float64).sum())}),
           flush=True)
     dist.destroy_process_group()

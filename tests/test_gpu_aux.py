@@ -10,8 +10,8 @@ with the previous schedule (cv_latent_step after the decoder backward):
     adds per element in the other order; the remaining run-to-run spread is the fp32-atomic dz partials);
   * both match the fp64 oracle at the parity bar (1e-4 on the losses).
 Also with the merge switched off in the library (cv_debug_aux(0)): the queued phases launch on their own at the
-flush points, same results.  Both with the combine split (LATENT_CHAIN, default: its KL part rides in the rows-phase
-grid, the decoder-chain part in the heads backward — d(heads) in memory then lacks the chain term, which the test
+flush points, same results.  Both with the combine split (LATENT_CHAIN, opt-in — measured slower, engine.py keeps it
+off: its KL part rides in the rows-phase grid, the decoder-chain part in the heads backward — d(heads) in memory then lacks the chain term, which the test
 adds from z / dz / heads) and with the one-launch combine after the decoder backward; and with the gradient phase
 queued before the output-loss launch instead (LATENT_AUX_OUT, cv_output_loss serves it)."""
 

@@ -3,7 +3,7 @@ all-reduces inside, rehearsed on the one-GPU box in a world-1 `nccl` process gro
 CVHIP_FORCE_DP=1 so the buckets really go through RCCL).  Reference step: /root/reference/code/src/trainer.py:861-888
 (the VAE backward + Adam, then CLEAR-MIM's 5 estimator updates, each with its own gradient all-reduce under DDP).
 
-For CLEAR and CLEAR-MIM, 4 steps (one eager, three replayed) run with the captured form and with the
+For CLEAR and CLEAR-MIM, 6 steps (one eager, five replayed) run with the captured form and with the
 host-sequenced segments (graphs between host-issued all-reduces, the default):
   * the captured form really built one graph for the step (and the default one per segment);
   * losses of every step agree to 1e-4 relative and the final parameter / Adam-state arenas to 1e-6 (the
@@ -33,8 +33,11 @@ def _free_port():
 
 
 def _run(mode, captured):
-    env = dict(os.environ, CVHIP_FORCE_DP="1", CVHIP_GRAPH_COLLECTIVES="1" if captured else "0")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "graph_coll_worker.py"), mode, "4",
+    # the default group keeps the event cache ON (torch's default, set explicitly): the round-5 abort needed it
+    # off, through a helper the caller had to remember; the engine now captures on a group of its own
+    env = dict(os.environ, CVHIP_FORCE_DP="1", CVHIP_GRAPH_COLLECTIVES="1" if captured else "0",
+               TORCH_NCCL_CUDA_EVENT_CACHE="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "graph_coll_worker.py"), mode, "6",
                         str(_free_port())], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -44,8 +47,8 @@ def _run(mode, captured):
 def test_captured_collectives_match_host_sequenced(mode):
     a = _run(mode, True)
     b = _run(mode, False)
-    assert a["capture"] and a["one_graph"] and a["ngraphs"] == 1, a
-    assert not b["capture"] and not b["one_graph"] and b["ngraphs"] > 1, b
+    assert a["capture"] and a["one_graph"] and a["ngraphs"] == 1 and a["own_group"], a
+    assert not b["capture"] and not b["one_graph"] and b["ngraphs"] > 1 and not b["own_group"], b
     def close(u, v, tol=1e-5):
         return abs(u - v) <= tol * max(abs(v), 1e-3)
 
