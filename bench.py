@@ -182,7 +182,8 @@ def isolated_pass(G, reps=20, rounds=3):
     times = {}
     for pname, P in _programs(G):
         for i, (name, fn, args, _lane) in enumerate(P.calls):
-            if fn is None or name in ("cv_ntxent_aux", "cv_ntxent_aux_combine", "cv_ntxent_aux_flush"):  # (a join; a queue)
+            if (fn is None or _lane in ("join", "host")
+                    or name in ("cv_ntxent_aux", "cv_ntxent_aux_combine", "cv_ntxent_aux_flush")):  # (a join; a queue)
                 continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):

@@ -447,6 +447,13 @@ def ensure_gemm_workspace(device) -> None:
     _GEMM_WS[idx] = buf
 
 
+def gemm_workspace(device) -> torch.Tensor:
+    """The device's registered GEMM workspace (ensure_gemm_workspace)."""
+    ensure_gemm_workspace(device)
+    device = torch.device(device)
+    return _GEMM_WS[device.index if device.index is not None else torch.cuda.current_device()]
+
+
 def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
 

@@ -98,6 +98,13 @@ LATENT_AUX_OUT = os.environ.get("CVHIP_LATENT_AUX_OUT", "0") == "1"
 # the combine launch it replaces, and the KL workgroup lengthened the rows-phase grid by 12 us).
 LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 
+# CVHIP_MIM_BRANCHES (default 2; 0: the sequential form): CLEAR-MIM's five estimator-update decoder forwards
+# (trainer.py:873-888) on this many side lanes of the single-GPU step graph, beside the five estimator learning steps
+# on the step's stream (ClearStep._programs, make_learn_branched).  Measured (round 6, VAE64 n = 256, the five
+# decoder forwards alone in a graph, scratch experiment): back to back 1.50 ms; on 5 / 3 / 2 lanes 1.23 / 1.20 /
+# 1.25 ms; one decoder pass over 5 x 256 images (the bound of a segmented-statistics kernel) 1.27 ms.
+MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "2"))
+
 
 def disc_params(disc):
     """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
@@ -547,6 +554,52 @@ class ClearStep:
                            E.numel, self.est_adam.hyper, self.est_adam.step)
                 return lp
 
+            # MIM_BRANCHES > 0: the five decoder forwards are independent of each other and of the estimator (update j
+            # reads only z_j, and its decoder pass only feeds the running statistics), so once the encoder pass has
+            # run and the five z_j are drawn in order on the step's stream (the noise of the sequential form, draw by
+            # draw), update j's decoder forward runs on side lane 1 + j % MIM_BRANCHES of the graph with its own
+            # activations, statistics and in-launch split-K workspace, while the step's stream runs the five
+            # estimator learning steps (each needs only z_j and the previous step's estimator); after the join the
+            # running statistics take their five momentum updates in order, as five forwards would have.
+            nbr = MIM_BRANCHES
+            if nbr > 0:
+                bws = [ws] + [Workspace(sp, n, self.device, with_grad=False, encoder=False) for _ in range(4)]
+                nb_fix = int(_lib.lib().cv_gemm_workspace_bytes())
+                fixws = [torch.zeros((nb_fix + 15) // 16 * 4, dtype=torch.float32, device=self.device)
+                         for _ in range(nbr)]
+                dflt_fix = _lib.gemm_workspace(self.device)
+                set_fix = lambda buf: _lib.call("cv_set_gemm_workspace", buf.data_ptr(), buf.numel() * 4)  # noqa: E731
+
+            def make_learn_branched(inject: bool):
+                lp = Program()
+                # the VAE Adam step just moved the weights; the same launch zeroes every update's statistics
+                pack_program(sp, lp, "all", zero=[(w.stats, w.stats.numel() * 8) for w in bws])
+                rp = (eps_buf[1] if inject else None, self.seed, self.offset)
+                zs = [ws.z] + [w.z for w in bws[1:]]
+                if not ws.encoder_program(lp, X, True, reparam=rp):  # (z_0 drawn by the heads launch, or here)
+                    lp.add("cv_reparam_forward", ws.heads, n, d, rp[0], ctypes.c_uint64(self.seed), self.offset,
+                           zs[0], None)
+                for j in range(1, 5):
+                    lp.add("cv_reparam_forward", ws.heads, n, d, eps_buf[1 + j] if inject else None,
+                           ctypes.c_uint64(self.seed), None if inject else self.offset, zs[j], None)
+                for j in range(5):
+                    lane = 1 + j % nbr
+                    br = Program()
+                    bws[j].decoder_program(br, zs[j], True, "none")
+                    lp.add_host("gemm_workspace", set_fix, fixws[lane - 1])
+                    lp.extend(br, lane=lane)
+                lp.add_host("gemm_workspace", set_fix, dflt_fix)
+                for j in range(5):
+                    zj = zs[j].data_ptr()
+                    lp.add("cv_mi_learning_step", mlp, zj, 2 * d, zj + 4 * d, 2 * d, n, ws.mi_work,
+                           self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
+                           E.numel, self.est_adam.hyper, self.est_adam.step)
+                lp.add_join()
+                for j in range(5):
+                    ws.running_program(lp, ws.bn_enc + [bws[j].bn_1d] + bws[j].bn_dec)
+                lp.keep += fixws + bws[1:]
+                return lp
+
             def make_learn_dp(inject: bool):
                 # per estimator update: (forward + learning-loss gradients, Adam) with the estimator
                 # gradient all-reduced in between
@@ -567,6 +620,8 @@ class ClearStep:
 
             if self.dp:
                 learn, learn_inj = make_learn_dp(False), make_learn_dp(True)
+            elif nbr > 0:
+                learn, learn_inj = make_learn_branched(False), make_learn_branched(True)
             else:
                 learn, learn_inj = make_learn(False), make_learn(True)
         if self.mode == "tc":

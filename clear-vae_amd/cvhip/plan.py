@@ -414,27 +414,34 @@ SIDE_STREAM = os.environ.get("CVHIP_SIDE_STREAM", "0") == "1"
 LIN_MMA = _lib.MMA_FP32
 
 
-def _side_stream(device) -> "torch.cuda.Stream":
-    key = torch.device(device).index
+def _side_stream(device, k: int = 1) -> "torch.cuda.Stream":
+    """Side stream k (>= 1) of the device: one ordered queue per k, shared by every program."""
+    key = (torch.device(device).index, k)
     st = _SIDE_STREAMS.get(key)
     if st is None:
         st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
     return st
 
 
+JOIN = "join"  # lane of an explicit join entry
+HOST = "host"  # lane of a host-side call (no stream: e.g. selecting a launch workspace while the calls are enqueued)
+
+
 class Program:
     """A fixed list of C-ABI calls (the stream is supplied at run time).
 
-    Calls added with ``add_side`` run on a second stream: each forks from the main stream after the
-    main-stream calls issued before it (an event), consecutive side calls stay ordered among
-    themselves, and the main stream joins the side stream at the end of the program.  The backward
-    programs put the weight-gradient GEMMs there, so they overlap the next layer's data-gradient
-    GEMM instead of queueing behind it (both only read what the fork point has completed)."""
+    Each call has a lane: 0 is the stream the program runs on; k >= 1 is side stream k.  A side call forks from the
+    main stream after the main-stream calls issued before it (an event), calls of one side lane stay ordered among
+    themselves, and the main stream joins every side lane it forked at the end of the program (or at an explicit
+    join).  ``add_side`` puts the backward programs' weight-gradient GEMMs on side lane 1 (CVHIP_SIDE_STREAM=1), so
+    they overlap the next layer's data-gradient GEMM instead of queueing behind it (both only read what the fork
+    point has completed); ``extend(other, lane=k)`` runs a whole program on side lane k (CLEAR-MIM's estimator decoder
+    forwards, cvhip/engine.py).  Host entries (lane HOST) call a Python function at enqueue time."""
 
     def __init__(self):
         self.calls = []  # (name, fn, args, lane)
         self.keep = []  # keep ctypes structs alive
-        self._events = None
+        self._events = []
         self.join_at_end = True
 
     def _conv(self, args):
@@ -456,21 +463,29 @@ class Program:
         self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1 if SIDE_STREAM else 0))
 
     def add_fork(self, name: str, *args):
-        """A call on the side stream regardless of CVHIP_SIDE_STREAM (it forks from the main-stream calls before
+        """A call on side lane 1 regardless of CVHIP_SIDE_STREAM (it forks from the main-stream calls before
         it; a later add_join, in this or a later program, joins it back)."""
         self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1))
 
     def add_join(self):
-        """The main stream waits here for everything issued on the side stream so far."""
-        self.calls.append(("join", None, [], 2))
+        """The main stream waits here for everything issued on the side lanes so far."""
+        self.calls.append((JOIN, None, [], JOIN))
 
-    def extend(self, other: "Program"):
-        self.calls += other.calls
+    def add_host(self, name: str, fn, *args):
+        """fn(*args) on the host when the program is enqueued (eagerly, or while a graph is captured)."""
+        self.calls.append((name, fn, list(args), HOST))
+
+    def extend(self, other: "Program", lane: int | None = None):
+        """Append other's calls; lane=k moves its stream calls onto side lane k."""
+        if lane is None:
+            self.calls += other.calls
+        else:
+            self.calls += [(nm, fn, a, lane if isinstance(ln, int) else ln) for nm, fn, a, ln in other.calls]
         self.keep += other.keep
 
     def run(self, stream: int | None = None, join: bool | None = None, timer: list | None = None):
-        """join=False leaves the side stream running past the end of the program (a later program's
-        run joins it: the side stream is one ordered queue); graph capture needs a join before its end.
+        """join=False leaves the side lanes running past the end of the program (a later program's
+        run joins them: each side lane is one ordered queue); graph capture needs a join before its end.
         timer (eager measurement only, bench.py): a list that receives (call index, start, end) timing
         events recorded around each call on the stream the call runs on."""
         try:
@@ -480,6 +495,12 @@ class Program:
             # pointers: drop it, so the next queue or served launch does not issue it
             _lib.lib().cv_ntxent_aux_discard()
             raise
+
+    def _event(self, i):
+        # (created on the first, eager run and reused by graph capture: the call sequence is fixed)
+        while len(self._events) <= i:
+            self._events.append(torch.cuda.Event())
+        return self._events[i]
 
     def _run(self, stream, join, timer):
         s = _lib.stream_handle() if stream is None else stream
@@ -496,37 +517,54 @@ class Program:
                     e1.record(main)
                     timer.append((i, e0, e1))
             return
-        side = _side_stream(main.device)
-        if self._events is None:  # created on the first (eager) run, reused by graph capture
-            nf = sum(1 for i, c in enumerate(self.calls) if c[3] == 1 and (i == 0 or self.calls[i - 1][3] != 1))
-            nj = sum(1 for c in self.calls if c[3] == 2)
-            self._events = [torch.cuda.Event() for _ in range(nf + nj + 1)]
         ev = 0
-        prev_lane = 0
+        forked = {}  # side lane -> forked since the main stream's last call (no new fork needed)
+        active = []  # side lanes forked in this run, not yet joined
+
+        def join_all():
+            nonlocal ev
+            # (a join with no side lane forked in this run joins side lane 1: a fork left open by an earlier
+            # program, join_at_end=False)
+            for k in (active or [1]):
+                e = self._event(ev)
+                ev += 1
+                e.record(_side_stream(main.device, k))
+                main.wait_event(e)
+            active.clear()
+            forked.clear()
+
         for i, (name, fn, args, lane) in enumerate(self.calls):
-            if lane == 2:  # explicit join: the main stream waits for the side stream's work so far
-                self._events[ev].record(side)
-                main.wait_event(self._events[ev])
-                ev += 1
-                prev_lane = 0
+            if lane == JOIN:
+                join_all()
                 continue
-            if lane and not prev_lane:  # fork: the side stream waits for the main-stream work so far
-                self._events[ev].record(main)
-                side.wait_event(self._events[ev])
-                ev += 1
+            if lane == HOST:
+                fn(*args)
+                continue
+            if lane:
+                side = _side_stream(main.device, lane)
+                if not forked.get(lane):  # fork: the side lane waits for the main-stream work so far
+                    e = self._event(ev)
+                    ev += 1
+                    e.record(main)
+                    side.wait_event(e)
+                    forked[lane] = True
+                    if lane not in active:
+                        active.append(lane)
+                st, h = side, side.cuda_stream
+            else:
+                forked.clear()  # (main-stream work after this point: a later side call forks again)
+                st, h = main, s
             if timer is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(side if lane else main)
-            rc = fn(*args, side.cuda_stream if lane else s)
+                e0.record(st)
+            rc = fn(*args, h)
             if rc != 0:
                 _lib.check(rc, name)
             if timer is not None:
-                e1.record(side if lane else main)
+                e1.record(st)
                 timer.append((i, e0, e1))
-            prev_lane = lane
-        if self.join_at_end if join is None else join:
-            self._events[ev].record(side)
-            main.wait_event(self._events[ev])
+        if (self.join_at_end if join is None else join) and active:
+            join_all()
 
 
 class DeferGroup:
@@ -563,12 +601,14 @@ def ptr_array(ptrs):
 class Workspace:
     """Device buffers of one batch size for one model (all NHWC fp32 unless noted)."""
 
-    def __init__(self, spec: VaeSpec, n: int, device, with_grad: bool = True):
+    def __init__(self, spec: VaeSpec, n: int, device, with_grad: bool = True, encoder: bool = True):
+        """encoder=False: no encoder activations (a workspace that only decodes a given z: CLEAR-MIM's estimator
+        decoder forwards)."""
         self.spec, self.n, self.device = spec, n, device
         _lib.ensure_gemm_workspace(device)
         f32 = dict(dtype=torch.float32, device=device)
         d = spec.d
-        self.y_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out, **f32) for c in spec.enc]
+        self.y_enc = [torch.empty(n * c.h_out * c.w_out * c.c_out if encoder else 0, **f32) for c in spec.enc]
         self.heads = torch.empty(n, 4 * d, **f32)
         self.z = torch.empty(n, 2 * d, **f32)
         self.h = torch.empty(n, spec.dec_lin.out_features, **f32)
@@ -763,9 +803,10 @@ class Workspace:
         P.add("cv_reparam_forward", self.heads, self.n, self.spec.d, eps.data_ptr() if eps is not None else None,
               ctypes.c_uint64(seed), offset.data_ptr() if offset is not None else None, self.z, None)
 
-    def running_program(self, P: Program, which: str = "all", side: bool = False):
-        """side=True: on the side stream (only where nothing re-zeroes the statistics before a join)."""
-        views = {"all": self.bnv, "enc": self.bn_enc, "dec": [self.bn_1d] + self.bn_dec}[which]
+    def running_program(self, P: Program, which="all", side: bool = False):
+        """side=True: on the side stream (only where nothing re-zeroes the statistics before a join).  which: a
+        name ('all', 'enc', 'dec') or an explicit list of BNViews (possibly of several workspaces)."""
+        views = self._views(which)
         bns = struct_array(cv_bn, [b.cv(True) for b in views])
         nbt = ptr_array([b.mod.num_batches_tracked.data_ptr() for b in views])
         (P.add_side if side else P.add)("cv_bn_update_running", bns, len(views),
