@@ -657,9 +657,14 @@ struct PackArgs {
   long zstart[9];  // prefix sums of 4-byte words (zvec: of 16-byte units)
   int zn;
   int zvec;        // every zeroed buffer 16-byte aligned and sized: 16-byte stores
+  // copies done by the same slice (cv_pack_conv_weights_zero_copy: the step's input batch), 16-byte units
+  uint4* cd[4];
+  const uint4* csrc[4];
+  long cstart[5];
+  int cn;
 };
 
-// blockIdx.y == a.n: zero the listed buffers (grid-stride over blockIdx.x)
+// blockIdx.y == a.n: zero the listed buffers and do the listed copies (grid-stride over blockIdx.x)
 __device__ __forceinline__ void pack_zero_slice(const PackArgs& a) {
   const long total = a.zstart[a.zn];
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -667,6 +672,12 @@ __device__ __forceinline__ void pack_zero_slice(const PackArgs& a) {
     while (b + 1 < a.zn && i >= a.zstart[b + 1]) ++b;
     if (a.zvec) reinterpret_cast<uint4*>(a.zp[b])[i - a.zstart[b]] = make_uint4(0u, 0u, 0u, 0u);
     else a.zp[b][i - a.zstart[b]] = 0u;
+  }
+  const long ctot = a.cstart[a.cn];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ctot; i += (long)gridDim.x * 256) {
+    int b = 0;
+    while (b + 1 < a.cn && i >= a.cstart[b + 1]) ++b;
+    a.cd[b][i - a.cstart[b]] = a.csrc[b][i - a.cstart[b]];
   }
 }
 // small layers: one destination element per thread, each destination walked in its own order
@@ -1469,11 +1480,21 @@ CV_STAMPS_SETTER(cv_debug_set_stamps)
 #endif
 
 static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, const size_t* zbytes, int zcount,
-                       cv_stream_t stream) {
+                       cv_stream_t stream, void* const* cdst = nullptr, const void* const* csrc = nullptr,
+                       const size_t* cbytes = nullptr, int ccount = 0) {
   CV_REQUIRE(items && n > 0 && n <= MAX_PACK, "pack_conv_weights: 1..%d items", MAX_PACK);
   CV_REQUIRE(zcount >= 0 && zcount <= 8 && (!zcount || (zptrs && zbytes)), "pack_conv_weights: 0..8 zeroed buffers");
+  CV_REQUIRE(ccount >= 0 && ccount <= 4 && (!ccount || (cdst && csrc && cbytes)), "pack_conv_weights: 0..4 copies");
   PackArgs a;
   memset(&a, 0, sizeof(a));
+  a.cn = ccount;
+  for (int i = 0; i < ccount; ++i) {
+    CV_REQUIRE(cdst[i] && csrc[i] && cbytes[i] % 16 == 0 && (((uintptr_t)cdst[i] | (uintptr_t)csrc[i]) & 15) == 0,
+               "pack_conv_weights: copy %d not 16-byte aligned and sized", i);
+    a.cd[i] = (uint4*)cdst[i];
+    a.csrc[i] = (const uint4*)csrc[i];
+    a.cstart[i + 1] = a.cstart[i] + (long)(cbytes[i] / 16);
+  }
   a.zn = zcount;
   a.zvec = 1;
   for (int i = 0; i < zcount; ++i) {
@@ -1507,13 +1528,14 @@ static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, con
     gx = t > gx ? t : gx;
   }
   if (!tiled) gx = (mx + 255) / 256;
-  if (zcount) {  // (the zero slice walks its buffers grid-stride, ~4 units per thread: it widens the grid only as far
-                 // as that needs, so the small layers' rows of the grid are not mostly empty workgroups)
-    const long zg = (a.zstart[zcount] + 1023) / 1024;
+  if (zcount || ccount) {  // (the zero / copy slice walks its buffers grid-stride, ~4 units per thread: it widens the
+                           // grid only as far as that needs, so the small layers' rows of the grid are not mostly
+                           // empty workgroups)
+    const long zg = (a.zstart[zcount] + a.cstart[ccount] + 1023) / 1024;
     gx = zg > gx ? zg : gx;
   }
   if (gx > 1024) gx = 1024;
-  const dim3 grid((int)gx, n + (zcount ? 1 : 0));
+  const dim3 grid((int)gx, n + ((zcount || ccount) ? 1 : 0));
   if (tiled) hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, S(stream), a);
   else hipLaunchKernelGGL(pack_small_kernel, grid, dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("pack_conv_weights");
@@ -1529,6 +1551,14 @@ extern "C" int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void*
                                          const size_t* zero_bytes, int zero_count, cv_stream_t stream) {
   clear_error();
   return pack_launch(items, n, zero_ptrs, zero_bytes, zero_count, stream);
+}
+
+extern "C" int cv_pack_conv_weights_zero_copy(const cv_conv_pack* items, int n, void* const* zero_ptrs,
+                                              const size_t* zero_bytes, int zero_count, void* const* copy_dst,
+                                              const void* const* copy_src, const size_t* copy_bytes, int copy_count,
+                                              cv_stream_t stream) {
+  clear_error();
+  return pack_launch(items, n, zero_ptrs, zero_bytes, zero_count, stream, copy_dst, copy_src, copy_bytes, copy_count);
 }
 
 extern "C" int cv_conv_forward(const cv_conv* g, const cv_operand* in, const float* wpacked, const float* bias,

@@ -105,6 +105,11 @@ LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 # 1.25 ms; one decoder pass over 5 x 256 images (the bound of a segmented-statistics kernel) 1.27 ms.
 MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "2"))
 
+# CVHIP_PACK_COPY (default 1): a replayed step's first launch (weight packing + step zeroing) is issued eagerly before
+# the step graph with the batch copy folded in (cv_pack_conv_weights_zero_copy); 0: the packing is the graph's first
+# node and the copy a launch of its own (A/B)
+PACK_COPY = os.environ.get("CVHIP_PACK_COPY", "1") == "1"
+
 
 def disc_params(disc):
     """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
@@ -432,6 +437,13 @@ class ClearStep:
             return f
 
         fwd, fwd_inj = make_fwd(False), make_fwd(True)
+        # the replayed step's graph starts after the pack + zero launch: step() issues that launch eagerly with the
+        # batch copy into X / lab folded in (cv_pack_conv_weights_zero_copy: one launch instead of two)
+        pack_call = fwd.calls[0]
+        assert pack_call[0] == "cv_pack_conv_weights_zero", pack_call[0]
+        fwd_g = Program()
+        fwd_g.calls = fwd.calls[1:]
+        fwd_g.keep = fwd.keep
         # decoder backward (bucket 1 of the gradient arena).  Weight gradients are deferred: their split-K
         # partial tiles, the BN affine gradients and the running statistics are reduced by one
         # cv_step_reduce launch at the end of the backward (data parallel: one per gradient bucket, before
@@ -582,18 +594,31 @@ class ClearStep:
                 for j in range(1, 5):
                     lp.add("cv_reparam_forward", ws.heads, n, d, eps_buf[1 + j] if inject else None,
                            ctypes.c_uint64(self.seed), None if inject else self.offset, zs[j], None)
+                # per lane: its decoder forwards (lanes 1..nbr) or the five learning steps (lane nbr + 1); every lane
+                # forks once, after the draws.  The calls are enqueued round-robin over the lanes, so the graph's nodes
+                # are created (and submitted at each launch) interleaved and no lane's first kernel waits behind
+                # another lane's whole chain (a multi-queue graph launch submits its nodes at ~25 us each, measured)
+                lanes = {k: [] for k in range(1, nbr + 2)}
                 for j in range(5):
-                    lane = 1 + j % nbr
                     br = Program()
                     bws[j].decoder_program(br, zs[j], True, "none")
-                    lp.add_host("gemm_workspace", set_fix, fixws[lane - 1])
-                    lp.extend(br, lane=lane)
-                lp.add_host("gemm_workspace", set_fix, dflt_fix)
+                    lp.keep += br.keep
+                    lanes[1 + j % nbr] += br.calls
                 for j in range(5):
                     zj = zs[j].data_ptr()
                     lp.add("cv_mi_learning_step", mlp, zj, 2 * d, zj + 4 * d, 2 * d, n, ws.mi_work,
                            self.learn.data_ptr() + 4 * j, G, E.flat, E.grad, self.est_adam.m, self.est_adam.v,
                            E.numel, self.est_adam.hyper, self.est_adam.step)
+                    nm, fn, a, _ = lp.calls.pop()
+                    lanes[nbr + 1].append((nm, fn, a, nbr + 1))
+                queues = {k: [(c[0], c[1], c[2], k) for c in v] for k, v in lanes.items()}
+                while any(queues.values()):
+                    for k, q in queues.items():
+                        if q:
+                            if k <= nbr:  # (each decoder lane's launches take that lane's split-K workspace)
+                                lp.add_host("gemm_workspace", set_fix, fixws[k - 1])
+                            lp.calls.append(q.pop(0))
+                lp.add_host("gemm_workspace", set_fix, dflt_fix)
                 lp.add_join()
                 for j in range(5):
                     ws.running_program(lp, ws.bn_enc + [bws[j].bn_1d] + bws[j].bn_dec)
@@ -650,7 +675,8 @@ class ClearStep:
 
             learn, learn_inj = make_tc(False), make_tc(True)
         return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, enc2=enc2, upd=upd, learn=learn,
-                    fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf)
+                    fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf,
+                    fwd_g=fwd_g, pack_call=pack_call)
 
     def _disc_struct(self) -> cv_tc_disc:
         l0w, l0b, l2w, l2b = self.est_arena.params
@@ -684,10 +710,11 @@ class ClearStep:
         mid = self.arena.offset[id(self.spec.enc[k].mod.weight)][0]
         return [(split, self.arena.numel), (mid, split), (0, mid)]
 
-    def _segments(self, G, inject=False):
+    def _segments(self, G, inject=False, graph=False):
         """The step as ('prog', [Program...]) segments and ('ar', bucket) / ('ar_est',) / ('wait',)
-        points (single GPU: one segment)."""
-        fwd = G["fwd_inj" if inject else "fwd"]
+        points (single GPU: one segment).  graph=True: the programs a step graph is captured from (the step's
+        first launch, pack + zero, is issued before the graph with the batch copy: _pack_and_load)."""
+        fwd = G["fwd_inj" if inject else ("fwd_g" if graph else "fwd")]
         lat = G["lat_inj" if inject else "lat"]
         learn = G["learn_inj" if inject else "learn"]
         if not self.dp:
@@ -764,7 +791,7 @@ class ClearStep:
         PyTorch's per-replay RNG bookkeeping); with capture_collectives, one graph for the whole data-parallel step,
         its all-reduces captured between the segments (the first, eager step has created the communicators)."""
         if self.capture_collectives:
-            def record_all(s, segs=self._segments(G, False)):
+            def record_all(s, segs=self._segments(G, False, graph=PACK_COPY)):
                 for item in segs:
                     kind = item[0]
                     if kind == "prog":
@@ -783,7 +810,7 @@ class ClearStep:
             G["one_graph"] = True
             return
         graphs = []
-        for item in self._segments(G, False):
+        for item in self._segments(G, False, graph=PACK_COPY):
             if item[0] != "prog":
                 continue
 
@@ -808,6 +835,27 @@ class ClearStep:
             G["X"].copy_(X, non_blocking=True)
             G["lab"].copy_(lab, non_blocking=True)
 
+    def _pack_and_load(self, G, X, label):
+        """The replayed step's first launch: the weight packing and step zeroing of the `fwd` program with the
+        batch copy into the graph's static inputs folded in (one launch), or the copy by torch and the packing on
+        its own when the batch needs a conversion."""
+        lab = label.reshape(-1)
+        name, fn, args, _ = G["pack_call"]
+        nbx, nbl = G["X"].numel() * 4, G["lab"].numel() * 8
+        if (X.dtype == torch.float32 and X.is_contiguous() and X.device == G["X"].device and lab.dtype == torch.int64
+                and lab.is_contiguous() and lab.device == G["lab"].device and X.numel() * 4 == nbx
+                and lab.numel() * 8 == nbl and nbx % 16 == 0 and nbl % 16 == 0
+                and (X.data_ptr() | lab.data_ptr()) % 16 == 0):
+            dst = ptr_array([G["X"].data_ptr(), G["lab"].data_ptr()])
+            src = ptr_array([X.data_ptr(), lab.data_ptr()])
+            nb = (ctypes.c_size_t * 2)(nbx, nbl)
+            _lib.call("cv_pack_conv_weights_zero_copy", *args, dst, src, nb, 2, _lib.stream_handle())
+            return
+        self._load_batch(G, X, label)
+        rc = fn(*args, _lib.stream_handle())
+        if rc != 0:
+            _lib.check(rc, name)
+
     def step(self, X, label, before_update=None):
         """One training step on the batch (X, label).  before_update: an optional callable run (on the host, in
         stream order: the step's kernels before it are enqueued, none after) once the gradients are complete —
@@ -826,11 +874,14 @@ class ClearStep:
         self.adam.refresh_hyper()
         if self.two_nets:
             self.est_adam.refresh_hyper()
-        self._load_batch(G, X, label)
         inject = self._take_injections(G)
         use_graph = G["count"] >= 1 and not inject and self.graphs_enabled and before_update is None
         if use_graph and "graphs" not in G:
             self._capture(G)
+        if use_graph and PACK_COPY:
+            self._pack_and_load(G, X, label)
+        else:
+            self._load_batch(G, X, label)
         if use_graph and G.get("one_graph"):
             G["graphs"][0].replay()  # (the whole step, collectives included: one launch)
         elif use_graph:

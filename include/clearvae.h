@@ -126,6 +126,12 @@ int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream);
  * touched by the packing: the first launch of a training step clears the step's accumulators with it. */
 int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void* const* zero_ptrs, const size_t* zero_bytes,
                               int zero_count, cv_stream_t stream);
+/* cv_pack_conv_weights_zero plus up to 4 device copies (16-byte aligned and sized) in the same launch: the fused
+ * step's first launch of a replayed step also moves the batch (X, labels: trainer.py:447-450's `X.to(device)` of a
+ * device-resident batch) into the step graph's static input buffers, so the copy is not a launch of its own. */
+int cv_pack_conv_weights_zero_copy(const cv_conv_pack* items, int n, void* const* zero_ptrs, const size_t* zero_bytes,
+                                   int zero_count, void* const* copy_dst, const void* const* copy_src,
+                                   const size_t* copy_bytes, int copy_count, cv_stream_t stream);
 
 /* y = conv(T(x)) + bias.  Replaces nn.Conv2d/ConvTranspose2d.forward (vae.py:15-46) with the
  * preceding BatchNorm2d+ReLU fused into the operand load and the following BatchNorm2d's batch
