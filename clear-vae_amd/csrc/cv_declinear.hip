@@ -24,6 +24,7 @@
 // Batch sums are accumulated in fp64 per lane and combined in a fixed order.
 #include <type_traits>
 #include "cv_common.hpp"
+#include "cv_ntxent.hpp"
 
 namespace cv {
 namespace dl {
@@ -134,8 +135,10 @@ struct FwdArgs {
 };
 
 // KR: K = 2d rounded up to a multiple of 16
+// (bx, gx: the workgroup's feature block and the number of blocks: its own blockIdx / gridDim, or its share of a
+// grid that also runs an NT-Xent phase, declinear_fwd_aux_kernel)
 template <int KR>
-__global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
+__device__ __forceinline__ void declinear_fwd_body(const FwdArgs& A, const int bx, const int gx) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int P = KR + 4;
   const int K = 2 * A.d, n = A.n, F = A.F, nt = (n + 15) >> 4;
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
   __shared__ double red[2][NTD / 64][DF];
   __shared__ BnFwdC kf[DF];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
-  const int col0 = blockIdx.x * DF, col = col0 + lr;
+  const int col0 = bx * DF, col = col0 + lr;
   const int f = feature_of(col, A.pix, A.ch);
   const uint64_t off = A.offset ? A.offset[0] : 0;
   // ---- B fragments: W[f][k] (k = 16 c + 4 lq + s), and the bias (requested first: used last)
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
         const float v1 = mu[u].y + ep[u].y * expf(0.5f * lv[u].y);
         sz[row * P + j] = v0;
         sz[row * P + j + 1] = v1;
-        if ((int)((p >> 6) % gridDim.x) == (int)blockIdx.x) {  // this workgroup's share of z
+        if ((int)((p >> 6) % gx) == bx) {  // this workgroup's share of z
           A.z[e] = v0;
           A.z[e + 1] = v1;
         }
@@ -254,12 +257,16 @@ __global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
     __syncthreads();
     if (t == 0) {
       const unsigned long long prev = atomicAdd((unsigned long long*)(A.offset + 1), 1ull);
-      if (prev == (unsigned long long)(gridDim.x - 1)) {
+      if (prev == (unsigned long long)(gx - 1)) {
         A.offset[0] = off + 1;
         A.offset[1] = 0;
       }
     }
   }
+}
+template <int KR>
+__global__ __launch_bounds__(NTD) void declinear_fwd_kernel(const FwdArgs A) {
+  declinear_fwd_body<KR>(A, blockIdx.x, gridDim.x);
 }
 
 struct BwdArgs {
@@ -280,7 +287,7 @@ struct BwdArgs {
 constexpr int TB = 4;  // 16-row tiles whose elementwise loads are in flight together (per wave)
 
 template <int KR>
-__global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
+__device__ __forceinline__ void declinear_bwd_body(const BwdArgs& A, const int bx) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int P = KR + 4;
   const int K = A.K, n = A.n, F = A.F, nt = (n + 15) >> 4;
@@ -291,11 +298,11 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
   __shared__ BnFwdC kf[DF];
   __shared__ BnBwdC kb[DF];
   const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lq = l >> 4;
-  const int col0 = blockIdx.x * DF, col = col0 + lr;
+  const int col0 = bx * DF, col = col0 + lr;
   // Row-tile order rotated by workgroup: every workgroup adds its dz partials onto the same [n][K] rows, so in a
   // common order all of them hit one 16-row block at a time; the wave offset and the slot rotation spread them over
   // NW TB blocks.  Register slot i holds tile tile0 + NW ((i + sr) % TB): static slots, rotated tiles.
-  const int wr = A.rot ? (w + (int)blockIdx.x) % NW : w, sr = A.rot ? ((int)blockIdx.x / NW) & (TB - 1) : 0;
+  const int wr = A.rot ? (w + bx) % NW : w, sr = A.rot ? (bx / NW) & (TB - 1) : 0;
   auto tile_at = [&](int tile0, int i) { return tile0 + NW * ((i + sr) & (TB - 1)); };
   auto load = [&](int tile0, float (*hv)[4], float (*dv)[4]) {
 #pragma unroll
@@ -430,6 +437,41 @@ __global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
     for (int ww = 0; ww < NTD / 64; ++ww) v += sred[(ww * DF + cl) * KR + kk];
     A.gw[(size_t)feature_of(col0 + cl, A.pix, A.ch) * K + kk] += v;
   }
+}
+template <int KR>
+__global__ __launch_bounds__(NTD) void declinear_bwd_kernel(const BwdArgs A) {
+  declinear_bwd_body<KR>(A, blockIdx.x);
+}
+
+// The decoder-input launches with an NT-Xent phase (cv_ntxent_aux) as extra workgroups of the same grid: the row
+// log-sum-exps in the forward's, the losses and gradients in the backward's.  Those grids hold one 512-thread
+// workgroup per 16 features (128 for both models' 2048 features): half the CUs are idle while they run, which the
+// NT-Xent workgroups take (the decoder ConvTranspose2d grids that served the phases before were full, and the
+// phases cost ~9 us each there in taken slots).  The feature blocks are dispatched first; an NT-Xent
+// workgroup runs the register-resident 256-thread body on its first four waves (waves 4..7 leave at once: a
+// barrier waits only on the waves still running).  Results are those of the standalone launches, bit for bit (the
+// same bodies on the same data).
+template <int KR, int DM, int JM>
+__global__ __launch_bounds__(NTD) void declinear_fwd_aux_kernel(const FwdArgs A, const NtArgs PA, const int nd,
+                                                                const int agx) {
+  const int v = blockIdx.x;
+  if (v < nd) {
+    declinear_fwd_body<KR>(A, v, nd);
+    return;
+  }
+  if (threadIdx.x >= 256) return;
+  ntxent_rows_reg_body<DM, JM>(PA, (v - nd) % agx, (v - nd) / agx);
+}
+template <int KR, int DM, int JM>
+__global__ __launch_bounds__(NTD) void declinear_bwd_aux_kernel(const BwdArgs A, const NtArgs PA, const int nd,
+                                                                const int agx) {
+  const int v = blockIdx.x;
+  if (v < nd) {
+    declinear_bwd_body<KR>(A, v);
+    return;
+  }
+  if (threadIdx.x >= 256) return;
+  ntxent_grad_reg_body<DM, JM>(PA, (v - nd) % agx, (v - nd) / agx);
 }
 
 // ---------------------------------------------------------------- encoder heads backward
@@ -782,6 +824,36 @@ static int pick_kr(int K, Fn fn) {
   return -1;
 }
 
+// CV_AUX_DL (default 1): a queued NT-Xent phase rides in the decoder-input launch that follows it (0: it stays queued
+// for its flush, A/B)
+static int aux_dl_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_AUX_DL");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+// The queued NT-Xent phase (cv_ntxent_aux) this decoder-input launch on stream st can serve as extra workgroups:
+// the merged kernel for (KR, phase) and the phase's arguments, or nullptr (not served: it stays queued)
+template <int KR>
+static const void* aux_dl_pick(int phase, hipStream_t st, NtArgs& pa, int& agx) {
+  if (!g_aux.set || g_aux.phase != phase || g_aux.stream != st || !aux_dl_on() || !aux_enabled()) return nullptr;
+  pa = g_aux.a;
+  if (pa.with_combine || !ntxent_reg_ok(pa, pa.nbr)) return nullptr;
+  const bool d8 = pa.d <= 8, d32 = pa.d <= 32 && pa.n <= 256;
+  const void* fn = nullptr;
+  if constexpr (KR == 16) {
+    if (d8) fn = phase == 0 ? (const void*)declinear_fwd_aux_kernel<16, 8, NTR_JM> : (const void*)declinear_bwd_aux_kernel<16, 8, NTR_JM>;
+  } else if constexpr (KR == 32 || KR == 64) {
+    if (d32) fn = phase == 0 ? (const void*)declinear_fwd_aux_kernel<KR, 32, 4> : (const void*)declinear_bwd_aux_kernel<KR, 32, 4>;
+  }
+  if (!fn) return nullptr;
+  agx = (pa.n + pa.rpb - 1) / pa.rpb;
+  return fn;
+}
+
 static int set_lds(const void* kern, size_t bytes) {
   if (bytes <= 64 * 1024) return 0;
   if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
@@ -838,6 +910,24 @@ extern "C" int cv_decoder_input_forward(const cv_linear* g, const float* heads, 
     constexpr int KR = decltype(kr)::value;
     const size_t lds = (size_t)((g->n + 15) & ~15) * (KR + 4) * sizeof(float);
     const void* kern = (const void*)declinear_fwd_kernel<KR>;
+    NtArgs pa;
+    int agx = 0;
+    if (const void* fx = aux_dl_pick<KR>(0, S(stream), pa, agx)) {  // + the queued row log-sum-exps phase
+      if (!set_lds(fx, lds)) {
+        int nd = F / DF;
+        void* params[] = {&a, &pa, &nd, &agx};
+        g_aux.set = 0;
+        note_launch(fx);
+        if (hipLaunchKernel(fx, dim3((unsigned)(nd + agx * pa.nbr)), dim3(NTD), params, lds, S(stream)) != hipSuccess) {
+          (void)hipGetLastError();
+          set_error("decoder_input_forward + NT-Xent: launch failed");
+          return 2;
+        }
+        aux_count_merged();
+        return 0;
+      }
+      (void)hipGetLastError();
+    }
     if (set_lds(kern, lds)) {
       set_error("decoder_input_forward: LDS carve-out of %zu bytes refused", lds);
       return 1;
@@ -898,6 +988,24 @@ extern "C" int cv_decoder_input_backward(const cv_linear* g, float* ga, const fl
     const size_t fold = (size_t)(NTD / 64) * (DF * KR + 16 * 17);  // the weight-gradient fold + the dz transposes
     const size_t lds = ((size_t)((g->n + 15) & ~15) * (KR + 4) + fold) * sizeof(float);
     const void* kern = (const void*)declinear_bwd_kernel<KR>;
+    NtArgs pa;
+    int agx = 0;
+    if (const void* fx = aux_dl_pick<KR>(1, S(stream), pa, agx)) {  // + the queued losses / gradients phase
+      if (!set_lds(fx, lds)) {
+        int nd = F / DF;
+        void* params[] = {&a, &pa, &nd, &agx};
+        g_aux.set = 0;
+        note_launch(fx);
+        if (hipLaunchKernel(fx, dim3((unsigned)(nd + agx * pa.nbr)), dim3(NTD), params, lds, S(stream)) != hipSuccess) {
+          (void)hipGetLastError();
+          set_error("decoder_input_backward + NT-Xent: launch failed");
+          return 2;
+        }
+        aux_count_merged();
+        return 0;
+      }
+      (void)hipGetLastError();
+    }
     if (set_lds(kern, lds)) {
       set_error("decoder_input_backward: LDS carve-out of %zu bytes refused", lds);
       return 1;

@@ -98,6 +98,17 @@ LATENT_AUX_OUT = os.environ.get("CVHIP_LATENT_AUX_OUT", "0") == "1"
 # the combine launch it replaces, and the KL workgroup lengthened the rows-phase grid by 12 us).
 LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 
+# CVHIP_LATENT_AUX_DL (default 1; with LATENT_AUX, without LATENT_CHAIN / LATENT_AUX_OUT): the NT-Xent phases ride in
+# the decoder-input launches instead of the decoder ConvTranspose2d grids: the row log-sum-exps in the decoder-input
+# forward's grid, the losses and gradients in the decoder-input backward's (cv_declinear.hip
+# declinear_*_aux_kernel).  Those grids hold 128 workgroups of 512 threads, so half the CUs are free for the phases;
+# the ConvTranspose2d grids serve only d <= 8 (a larger register phase spills there).  Taken where those grids do not
+# serve the phase (d > 8: every VAE64 config, register NT-Xent for d <= 32, n <= 256).  Measured (round 6, same box,
+# two rounds): CelebA 2.1276 -> 2.0994 ms (the two standalone NT-Xent launches, 17 + 25 us, hidden in the decoder-input
+# grids); on MNIST (d = 8) the ConvTranspose2d placement stays: there the phases cost ~2 us each, in the decoder-input
+# grids 6 + 4 us (0.4735 -> 0.4820 ms with them there: CVHIP_LATENT_AUX_DL=2 forces it).
+LATENT_AUX_DL = int(os.environ.get("CVHIP_LATENT_AUX_DL", "1"))
+
 # CVHIP_MIM_BRANCHES (default 2; 0: the sequential form): CLEAR-MIM's five estimator-update decoder forwards
 # (trainer.py:873-888) on this many side lanes of the single-GPU step graph, beside the five estimator learning steps
 # on the step's stream (ClearStep._programs, make_learn_branched).  Measured (round 6, VAE64 n = 256, the five
@@ -398,6 +409,10 @@ class ClearStep:
         aux_args = ([(br_arr, len(branches), lab, n, d, self.sim, tau_c, ph, 1) for ph in (0, 1)]
                     if aux_nt else None)
         chain_nt = aux_nt and LATENT_CHAIN and ws.fused_heads()
+        # the phases in the decoder-input launches (LATENT_AUX_DL): phase 0 queued before the forward one, phase 1
+        # before the backward one (each flushed right after its launch)
+        dl_nt = (aux_nt and (LATENT_AUX_DL == 2 or (LATENT_AUX_DL == 1 and d > 8)) and not chain_nt
+                 and not LATENT_AUX_OUT and ws.fused_decoder_input())
         hpf = lambda k, dflt: ctypes.c_float(float(hp.get(k, dflt)))
         aux_comb = ((ws.heads, ws.z, n, d, hpf("beta", 0), hpf("loc", 0), hpf("scale", 1), self.anneal, ws.dheads,
                      ws.losses) if chain_nt else None)
@@ -428,9 +443,10 @@ class ClearStep:
                 ws.decoder_program(f, ws.z, True, "loss", X, rec_scale=gscale_rec)
                 f.keep += [gwork, gscale_rec]
             else:
-                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp, aux=aux_args,
-                                   aux_combine=aux_comb,
-                                   aux_at=(0, len(sp.dec) - 1) if LATENT_AUX_OUT else None)
+                ws.decoder_program(f, ws.z, True, "loss", X, reparam=None if drew else rp,
+                                   aux=None if dl_nt else aux_args, aux_combine=aux_comb,
+                                   aux_at=(0, len(sp.dec) - 1) if LATENT_AUX_OUT else None,
+                                   aux_in=aux_args[0] if dl_nt else None)
                 if aux_nt:
                     f.keep.append(br_arr)
             # (the running statistics are folded at the end of the backward by cv_step_reduce)
@@ -451,7 +467,10 @@ class ClearStep:
         dp = self.dp
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
         dec = Program()
-        ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer)
+        ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer,
+                                    aux_in=aux_args[1] if dl_nt else None)
+        if dl_nt:
+            dec.keep.append(br_arr)
         if dp:
             ws.step_reduce_program(dec, dec_defer, pg, "dec", running=False)
 

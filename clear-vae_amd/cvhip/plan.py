@@ -836,13 +836,14 @@ class Workspace:
         return self.FUSED_HEADS and bool(_lib.lib().cv_heads_backward_supported(self.n, sp.F, C, 4 * sp.d))
 
     def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None,
-                        aux=None, aux_combine=None, aux_at=None):
+                        aux=None, aux_combine=None, aux_at=None, aux_in=None):
         """reparam = (eps, seed, offset): z is drawn from self.heads first (cv_reparam_forward, or inside the
         fused decoder-input launch); None: z is given.  aux: cv_ntxent_aux argument tuples, the i-th queued before
         the i-th decoder conv (its phase rides in that launch where served) and flushed right after it — or
         before the decoder conv aux_at[i] (the last one: the output-loss call, whose loss launch serves a gradient
         phase); aux_combine: cv_ntxent_aux_combine arguments attached to the first (the KL part of the latent
-        combine)."""
+        combine); aux_in: cv_ntxent_aux arguments queued before the decoder-input launch (which serves it) and
+        flushed after it."""
         sp, n = self.spec, self.n
         Cu, Hu, Wu = sp.unflat
         lin = cv_linear(n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
@@ -853,11 +854,18 @@ class Workspace:
                       ctypes.c_uint64(seed), offset.data_ptr() if offset is not None else None, z, None)
                 reparam = None
             eps, seed, offset = reparam if reparam is not None else (None, 0, None)
+            if aux_in is not None:
+                P.add("cv_ntxent_aux", *aux_in)
             P.add("cv_decoder_input_forward", lin, self.heads if reparam is not None else None,
                   eps.data_ptr() if eps is not None else None, ctypes.c_uint64(seed),
                   offset.data_ptr() if offset is not None else None, z, sp.dec_lin.weight, sp.dec_lin.bias,
                   self.bn_1d.cv(train), self.bn_1d.stat if train else None, self.h, self.ah)
+            if aux_in is not None:
+                P.add("cv_ntxent_aux_flush")
         else:
+            if aux_in is not None:  # (no fused decoder-input launch to serve it: its own launch)
+                P.add("cv_ntxent_aux", *aux_in)
+                P.add("cv_ntxent_aux_flush")
             if reparam is not None:
                 self.reparam_program(P, *reparam)
             ep = ep_fwd(self.bn_1d) if train else ep_none()
@@ -890,9 +898,11 @@ class Workspace:
         if output == "xhat":
             P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)
 
-    def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True, defer=None):
+    def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True, defer=None,
+                                 aux_in=None):
         """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to
-        dz_out [n, 2d] (zeroed + accumulated) and the decoder parameter gradients."""
+        dz_out [n, 2d] (zeroed + accumulated) and the decoder parameter gradients.  aux_in: cv_ntxent_aux arguments
+        queued before the decoder-input backward launch (which serves it) and flushed after it."""
         sp, n = self.spec, self.n
         L = len(sp.dec)
         for li in range(L - 1, -1, -1):
@@ -914,9 +924,16 @@ class Workspace:
         if self.fused_decoder_input():  # gah <- d(h) in place, weight gradient, BN1d backward sums, dz
             if zero_dz:
                 P.add("cv_zero", dz_out, dz_out.numel() * 4)
+            if aux_in is not None:
+                P.add("cv_ntxent_aux", *aux_in)
             P.add("cv_decoder_input_backward", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
                   self.z, param_grad(sp.dec_lin.weight), sp.dec_lin.weight, dz_out)
+            if aux_in is not None:
+                P.add("cv_ntxent_aux_flush")
             return
+        if aux_in is not None:  # (no fused decoder-input launch to serve it: its own launch)
+            P.add("cv_ntxent_aux", *aux_in)
+            P.add("cv_ntxent_aux_flush")
         else:
             P.add("cv_declinear_backward_weight", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
                   self.z, param_grad(sp.dec_lin.weight))
