@@ -672,11 +672,12 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
 #pragma unroll
   for (int j = 0; j < CB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
   const int tot = (yb1 - yb0) * g.wb * CB;
-  float* dst = P.out + (size_t)(n * g.hb + yb0) * g.wb * CB;
+  // (P.out == nullptr: the statistics only, no output tensor — cv_conv_forward with out = NULL)
+  float* dst = P.out ? P.out + (size_t)(n * g.hb + yb0) * g.wb * CB : nullptr;
   const int tot4 = tot >> 2;
   for (int i = t; i < tot4; i += ET) {
     const f32x4 v = lds4(sOut + 4 * i);
-    *reinterpret_cast<f32x4*>(dst + 4 * i) = v;
+    if (dst) *reinterpret_cast<f32x4*>(dst + 4 * i) = v;
     if (mode == CV_STAT_FWD) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -689,7 +690,7 @@ __global__ __launch_bounds__(ET, OUT ? 4 : 1) void edge_scatter_kernel(const EAr
   }
   for (int i = 4 * tot4 + t; i < tot; i += ET) {
     const float v = sOut[i];
-    dst[i] = v;
+    if (dst) dst[i] = v;
     if (mode == CV_STAT_FWD) {
       const int j = i % CB;
 #pragma unroll

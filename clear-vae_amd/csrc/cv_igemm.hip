@@ -1179,9 +1179,11 @@ static int run_scatter(const Geo& g, const cv_operand* in, const float* w, const
   if (!g_force_generic) {
     const int er = edge_scatter(g, in, w, bias, out, ep, st);
     if (er >= 0) return er;
+    CV_REQUIRE(out, "%s: statistics-only output (out = NULL) is served by the image-side edge scatter only", what);
     const int dr = direct_scatter(g, in, g_wk, bias, out, ep, st, mma);
     if (dr >= 0) return dr;
   }
+  CV_REQUIRE(out, "%s: statistics-only output (out = NULL) is served by the image-side edge scatter only", what);
   const int nr = narrow_scatter(g, in, w, bias, out, ep, st);
   if (nr >= 0) return nr;
   Args a;
@@ -1565,7 +1567,11 @@ extern "C" int cv_conv_forward(const cv_conv* g, const cv_operand* in, const flo
                                float* out, const cv_epilogue* ep, cv_stream_t stream) {
   clear_error();
   if (check_conv(g) || check_operand(in, "conv_forward")) return 1;
-  CV_REQUIRE(wpacked && out, "conv_forward: null weight/out");
+  CV_REQUIRE(wpacked, "conv_forward: null weight");
+  // out == NULL: statistics only (the image-side ConvTranspose2d whose output is read by nothing but its BatchNorm's
+  // batch statistics: CLEAR-MIM's estimator forwards); served by the edge scatter alone
+  CV_REQUIRE(out || (ep && ep->stat_mode == CV_STAT_FWD && g->transposed), "conv_forward: null out needs a "
+             "ConvTranspose2d with the forward statistics epilogue");
   const Geo geo = geo_of(g);
   if (!g->transposed) return run_gather(geo, in, wpacked, bias, out, ep, S(stream), "conv_forward", g->mma);
   return run_scatter(geo, in, wpacked, bias, out, ep, S(stream), "convT_forward", g->mma);

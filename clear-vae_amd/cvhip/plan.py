@@ -835,6 +835,10 @@ class Workspace:
         C, Hh, Wh = sp.feat
         return self.FUSED_HEADS and bool(_lib.lib().cv_heads_backward_supported(self.n, sp.F, C, 4 * sp.d))
 
+    # CVHIP_STATS_ONLY_OUT (default 1): a train-mode decoder pass with output 'none' (CLEAR-MIM's estimator forwards,
+    # CLEAR-TC's discriminator forward) does not write the pre-BN image (0: it does, A/B)
+    STATS_ONLY_OUT = os.environ.get("CVHIP_STATS_ONLY_OUT", "1") != "0"
+
     def decoder_program(self, P: Program, z, train: bool, output: str, x=None, rec_scale=None, reparam=None,
                         aux=None, aux_combine=None, aux_at=None, aux_in=None):
         """reparam = (eps, seed, offset): z is drawn from self.heads first (cv_reparam_forward, or inside the
@@ -891,7 +895,11 @@ class Workspace:
                 if q is not None:
                     P.add("cv_ntxent_aux_flush")
                 return
-            P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, self.y_dec[li], ep)
+            # (a train-mode forward whose output is not wanted: the last ConvTranspose2d writes only its BatchNorm's
+            # batch statistics, not the pre-BN image — cv_conv_forward with out = NULL, the edge scatter)
+            stats_only = output == "none" and train and li == len(sp.dec) - 1 and self.STATS_ONLY_OUT
+            P.add("cv_conv_forward_kpack", g, op, c.wfwd, c.wbwd, c.mod.bias, None if stats_only else self.y_dec[li],
+                  ep)
             if q is not None:
                 P.add("cv_ntxent_aux_flush")
             cur = self.y_dec[li]
