@@ -900,6 +900,83 @@ extern "C" int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum
   return 0;
 }
 
+// Several forwards' momentum updates of the same layers in one launch, in order (CLEAR-MIM's five estimator forwards,
+// trainer.py:873-888: each `vae(X)` moves every BatchNorm's running statistics once): set s of layer l folds its own
+// batch sums; the thread (block) that owns a channel applies the sets one after the other.
+constexpr int MAX_SETS = 8;
+struct RunSetArgs {
+  cv_bn bn[MAX_BN];
+  const double* stat[MAX_SETS][MAX_BN];
+  int64_t* nbt[MAX_BN];
+  int nl, nsets;
+  float momentum;
+};
+__global__ __launch_bounds__(256) void bn_running_sets_kernel(const RunSetArgs a) {
+  __shared__ double scratch[4 * 256];
+  const int l = blockIdx.y;
+  if (l >= a.nl) return;
+  cv_bn b = a.bn[l];
+  float* rm = const_cast<float*>(b.running_mean);
+  float* rv = const_cast<float*>(b.running_var);
+  const float m = a.momentum;
+  auto update = [&](int c, double s, double q, double, double) {
+    const double n = (double)b.count;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const double unbiased = (b.count > 1) ? var * n / (n - 1.0) : var;
+    rm[c] = m * (float)mean + (1.0f - m) * rm[c];
+    rv[c] = m * (float)unbiased + (1.0f - m) * rv[c];
+  };
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.nbt[l]) a.nbt[l][0] += a.nsets;
+  if (b.C >= 256) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < b.C)
+      for (int st = 0; st < a.nsets; ++st) {
+        double s = 0.0, q = 0.0;
+        bn_sums(a.stat[st][l], b.C, c, s, q);
+        update(c, s, q, 0.0, 0.0);
+      }
+    return;
+  }
+  if (blockIdx.x != 0) return;
+  for (int st = 0; st < a.nsets; ++st) {
+    b.stat = a.stat[st][l];
+    bn_fold<256>(b, false, scratch, update);
+    __syncthreads();
+  }
+}
+
+extern "C" int cv_bn_update_running_sets(const cv_bn* bn, int nlayers, int nsets, float momentum,
+                                         int64_t* const* nbt, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(bn && nlayers > 0 && nlayers <= MAX_BN && nsets > 0 && nsets <= MAX_SETS,
+             "bn_update_running_sets: 1..%d layers x 1..%d sets", MAX_BN, MAX_SETS);
+  RunSetArgs a;
+  memset(&a, 0, sizeof(a));
+  int cmax = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    for (int st = 0; st < nsets; ++st) {
+      const cv_bn& x = bn[st * nlayers + i];
+      CV_REQUIRE(x.stat && x.running_mean && x.running_var && x.C > 0 && x.count > 0,
+                 "bn_update_running_sets: layer %d of set %d incomplete", i, st);
+      CV_REQUIRE(x.running_mean == bn[i].running_mean && x.running_var == bn[i].running_var && x.C == bn[i].C &&
+                     x.count == bn[i].count,
+                 "bn_update_running_sets: set %d's layer %d is another BatchNorm", st, i);
+      a.stat[st][i] = x.stat;
+    }
+    a.bn[i] = bn[i];
+    a.nbt[i] = nbt ? nbt[i] : nullptr;
+    cmax = bn[i].C > cmax ? bn[i].C : cmax;
+  }
+  a.nl = nlayers;
+  a.nsets = nsets;
+  a.momentum = momentum;
+  hipLaunchKernelGGL(bn_running_sets_kernel, dim3(cdiv(cmax, 256), nlayers), dim3(256), 0, S(stream), a);
+  CV_LAUNCH_CHECK("bn_update_running_sets");
+  return 0;
+}
+
 extern "C" int cv_bn_apply(const cv_bn* bn, const float* x, float* out, int rows, int features, int pix, int ch,
                            int relu, cv_stream_t stream) {
   clear_error();

@@ -662,19 +662,27 @@ struct PackArgs {
   const uint4* csrc[4];
   long cstart[5];
   int cn;
+  // flat 1-D grid: workgroups [wg0[l], wg0[l + 1]) pack layer l, the workgroups from wg0[n] on zero / copy
+  int wg0[MAX_PACK + 1];
 };
+// the layer of flat workgroup v (wg0 prefix sums; v >= wg0[n]: the zero / copy slice, returns n)
+__device__ __forceinline__ int pack_layer_of(const PackArgs& a, int v) {
+  int l = 0;
+  while (l < a.n && v >= a.wg0[l + 1]) ++l;
+  return l;
+}
 
-// blockIdx.y == a.n: zero the listed buffers and do the listed copies (grid-stride over blockIdx.x)
-__device__ __forceinline__ void pack_zero_slice(const PackArgs& a) {
+// the zero / copy slice: workgroup b of nb zeroes the listed buffers and does the listed copies (grid-stride)
+__device__ __forceinline__ void pack_zero_slice(const PackArgs& a, const long b, const long nb) {
   const long total = a.zstart[a.zn];
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+  for (long i = b * 256 + threadIdx.x; i < total; i += nb * 256) {
     int b = 0;
     while (b + 1 < a.zn && i >= a.zstart[b + 1]) ++b;
     if (a.zvec) reinterpret_cast<uint4*>(a.zp[b])[i - a.zstart[b]] = make_uint4(0u, 0u, 0u, 0u);
     else a.zp[b][i - a.zstart[b]] = 0u;
   }
   const long ctot = a.cstart[a.cn];
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ctot; i += (long)gridDim.x * 256) {
+  for (long i = b * 256 + threadIdx.x; i < ctot; i += nb * 256) {
     int b = 0;
     while (b + 1 < a.cn && i >= a.cstart[b + 1]) ++b;
     a.cd[b][i - a.cstart[b]] = a.csrc[b][i - a.cstart[b]];
@@ -682,16 +690,17 @@ __device__ __forceinline__ void pack_zero_slice(const PackArgs& a) {
 }
 // small layers: one destination element per thread, each destination walked in its own order
 __global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
-  const int l = blockIdx.y;
+  const int v = blockIdx.x, l = pack_layer_of(a, v);
   if (l == a.n) {
-    pack_zero_slice(a);
+    pack_zero_slice(a, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
     return;
   }
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
   const int total = cs * cbn * kk;
   const float* __restrict__ src = a.src[l];
   const FDiv f_cs = FDiv::make(cs), f_cb = FDiv::make(cbn);
-  for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+  const int b = v - a.wg0[l], nb = a.wg0[l + 1] - a.wg0[l];
+  for (int j = b * 256 + threadIdx.x; j < total; j += nb * 256) {
     if (a.dg[l]) {  // [tap][cb][cs]
       const int q = f_cs.div(j), c_s = j - q * cs, tap = f_cb.div(q), c_b = q - tap * cbn;
       a.dg[l][j] = src[(c_s * cbn + c_b) * kk + tap];
@@ -709,9 +718,9 @@ __global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
 constexpr int PK_CS = 16, PK_CB = 32, PK_MAXK = 16;
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   __shared__ float tile[PK_CS * PK_CB * (PK_MAXK + 1)];
-  const int l = blockIdx.y;
+  const int v = blockIdx.x, l = pack_layer_of(a, v);
   if (l == a.n) {
-    pack_zero_slice(a);
+    pack_zero_slice(a, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
     return;
   }
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
@@ -719,7 +728,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   const int ntile = ((cs + PK_CS - 1) / PK_CS) * tcb;
   const float* __restrict__ src = a.src[l];
   const int pitch = kk + 1;  // odd: the column walks below hit distinct banks
-  for (int tile_id = blockIdx.x; tile_id < ntile; tile_id += gridDim.x) {
+  const int tb = v - a.wg0[l], tnb = a.wg0[l + 1] - a.wg0[l];
+  for (int tile_id = tb; tile_id < ntile; tile_id += tnb) {
     const int cs0 = (tile_id / tcb) * PK_CS, cb0 = (tile_id % tcb) * PK_CB;
     const int ncs = min(PK_CS, cs - cs0), ncb = min(PK_CB, cbn - cb0);
     const int run = ncb * kk;  // contiguous floats per cs row of the block
@@ -1523,21 +1533,26 @@ static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, con
   }
   a.n = n;
   bool tiled = mx >= 256 * 1024;  // big layers: the LDS-tiled transpose; small ones: more parallelism
-  long gx = 1;
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n; ++i)
     if (a.kk[i] > PK_MAXK) tiled = false;
-    const long t = (long)cdiv(a.cs[i], PK_CS) * cdiv(a.cb[i], PK_CB);
-    gx = t > gx ? t : gx;
+  // One flat grid: each layer gets exactly the workgroups it has work for (its tiles, or its elements / 256, capped
+  // at 1024), then the zero / copy slice (~4 16-byte units per thread).  (The 2-D grid of round 5 gave every layer the
+  // widest layer's row of workgroups: on VAE64 ~10k of its 11k workgroups found no tile and only took dispatch slots
+  // and their LDS.)
+  a.wg0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    long t = tiled ? (long)cdiv(a.cs[i], PK_CS) * cdiv(a.cb[i], PK_CB)
+                   : ((long)a.cs[i] * a.cb[i] * a.kk[i] + 255) / 256;
+    if (t > 1024) t = 1024;
+    a.wg0[i + 1] = a.wg0[i] + (int)t;
   }
-  if (!tiled) gx = (mx + 255) / 256;
-  if (zcount || ccount) {  // (the zero / copy slice walks its buffers grid-stride, ~4 units per thread: it widens the
-                           // grid only as far as that needs, so the small layers' rows of the grid are not mostly
-                           // empty workgroups)
-    const long zg = (a.zstart[zcount] + a.cstart[ccount] + 1023) / 1024;
-    gx = zg > gx ? zg : gx;
+  long zg = 0;
+  if (zcount || ccount) {
+    zg = (a.zstart[zcount] + a.cstart[ccount] + 1023) / 1024;
+    if (zg < 1) zg = 1;
+    if (zg > 1024) zg = 1024;
   }
-  if (gx > 1024) gx = 1024;
-  const dim3 grid((int)gx, n + ((zcount || ccount) ? 1 : 0));
+  const dim3 grid((unsigned)(a.wg0[n] + zg));
   if (tiled) hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, S(stream), a);
   else hipLaunchKernelGGL(pack_small_kernel, grid, dim3(256), 0, S(stream), a);
   CV_LAUNCH_CHECK("pack_conv_weights");

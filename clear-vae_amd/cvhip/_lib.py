@@ -245,6 +245,7 @@ _SIGS = {
     ),
     "cv_bn_apply": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cv_bn_update_running": (c_int, [_P(cv_bn), c_int, c_float, _P(c_void_p), c_void_p]),
+    "cv_bn_update_running_sets": (c_int, [_P(cv_bn), c_int, c_int, c_float, _P(c_void_p), c_void_p]),
     "cv_bn_batch_stats": (c_int, [_P(cv_bn), c_void_p, c_void_p, c_void_p]),
     "cv_output_forward": (c_int, [_P(cv_bn), c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "cv_output_loss": (

@@ -639,8 +639,7 @@ class ClearStep:
                             lp.calls.append(q.pop(0))
                 lp.add_host("gemm_workspace", set_fix, dflt_fix)
                 lp.add_join()
-                for j in range(5):
-                    ws.running_program(lp, ws.bn_enc + [bws[j].bn_1d] + bws[j].bn_dec)
+                ws.running_sets_program(lp, [ws.bn_enc + [bws[j].bn_1d] + bws[j].bn_dec for j in range(5)])
                 lp.keep += fixws + bws[1:]
                 return lp
 

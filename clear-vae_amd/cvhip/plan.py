@@ -803,6 +803,15 @@ class Workspace:
         P.add("cv_reparam_forward", self.heads, self.n, self.spec.d, eps.data_ptr() if eps is not None else None,
               ctypes.c_uint64(seed), offset.data_ptr() if offset is not None else None, self.z, None)
 
+    def running_sets_program(self, P: Program, sets):
+        """The momentum updates of several forwards in one launch, in order: sets = [list of BNViews], the same
+        layers in each (cv_bn_update_running_sets)."""
+        views0 = sets[0]
+        bns = struct_array(cv_bn, [b.cv(True) for views in sets for b in views])
+        nbt = ptr_array([b.mod.num_batches_tracked.data_ptr() for b in views0])
+        P.add("cv_bn_update_running_sets", bns, len(views0), len(sets), ctypes.c_float(float(views0[0].mod.momentum)),
+              nbt)
+
     def running_program(self, P: Program, which="all", side: bool = False):
         """side=True: on the side stream (only where nothing re-zeroes the statistics before a join).  which: a
         name ('all', 'enc', 'dec') or an explicit list of BNViews (possibly of several workspaces)."""

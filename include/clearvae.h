@@ -300,6 +300,12 @@ int cv_bn_apply(const cv_bn* bn, const float* x, float* out, int rows, int featu
 /* ---- BatchNorm running statistics (nn.BatchNorm*, momentum 0.1, unbiased running var) ---- */
 int cv_bn_update_running(const cv_bn* bn, int nlayers, float momentum,
                          int64_t* const* num_batches_tracked, cv_stream_t stream);
+/* nsets forwards' momentum updates of the same nlayers BatchNorms in one launch, applied in set order: bn is
+ * [nsets][nlayers] (set-major; layer i of every set names the same running buffers, count and C, with its own
+ * batch sums in .stat); num_batches_tracked advances by nsets (CLEAR-MIM's five estimator forwards,
+ * trainer.py:873-888). */
+int cv_bn_update_running_sets(const cv_bn* bn, int nlayers, int nsets, float momentum, int64_t* const* nbt,
+                              cv_stream_t stream);
 /* copy batch stats into (mean, invstd) float arrays (for tests / PyTorch-visible save_mean) */
 int cv_bn_batch_stats(const cv_bn* bn, float* mean, float* invstd, cv_stream_t stream);
 
