@@ -853,6 +853,8 @@ class ClearStep:
             G["X"].copy_(X, non_blocking=True)
             G["lab"].copy_(lab, non_blocking=True)
 
+    PACK_COPY_MAX = int(os.environ.get("CVHIP_PACK_COPY_MAX", str(4 << 20)))  # bytes
+
     def _pack_and_load(self, G, X, label):
         """The replayed step's first launch: the weight packing and step zeroing of the `fwd` program with the
         batch copy into the graph's static inputs folded in (one launch), or the copy by torch and the packing on
@@ -860,10 +862,12 @@ class ClearStep:
         lab = label.reshape(-1)
         name, fn, args, _ = G["pack_call"]
         nbx, nbl = G["X"].numel() * 4, G["lab"].numel() * 8
+        # (folded in for small batches only: the pack launch's workgroups hold a 35 KB LDS tile each, so a large copy
+        # — VAE64 bs = 256: 12.6 MB — runs slower inside it than as its own launch: CelebA +3 us, MNIST -3 us, measured)
         if (X.dtype == torch.float32 and X.is_contiguous() and X.device == G["X"].device and lab.dtype == torch.int64
                 and lab.is_contiguous() and lab.device == G["lab"].device and X.numel() * 4 == nbx
                 and lab.numel() * 8 == nbl and nbx % 16 == 0 and nbl % 16 == 0
-                and (X.data_ptr() | lab.data_ptr()) % 16 == 0):
+                and (X.data_ptr() | lab.data_ptr()) % 16 == 0 and nbx + nbl <= self.PACK_COPY_MAX):
             dst = ptr_array([G["X"].data_ptr(), G["lab"].data_ptr()])
             src = ptr_array([X.data_ptr(), lab.data_ptr()])
             nb = (ctypes.c_size_t * 2)(nbx, nbl)
