@@ -1331,7 +1331,11 @@ static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
   for (int cap : {0, 64})
     for (long tg : {0L, wgrad_pm_target(t64)}) {
       const WPlan w = wgrad_plan(M, N, K, split_k, cap, tg);
-      const size_t need = w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
+      size_t need = w.split > 1 ? (size_t)w.split * M * (N + 1) * sizeof(float) : 0;
+      // (the self-reducing form's fragment slabs: whole BM x BN tiles per split, bias column included)
+      const size_t slab = w.split > 1 ? (size_t)w.split * cdiv(M, w.BM) * w.BM * cdiv(N + 1, w.BN) * w.BN * sizeof(float)
+                                      : 0;
+      if (slab > need) need = slab;
       if (need > b) b = need;
     }
   return b;
@@ -1341,6 +1345,7 @@ static size_t wgrad_ws_bytes(int M, int N, long K, int split_k) {
 // tiles are left in the caller's workspace and their layout is recorded instead of launching the reduction;
 // cv_step_reduce later sums every deferred gradient of the step in one launch.
 static thread_local cv_wgrad_defer* g_defer_sink = nullptr;
+static int g_wgrad_self = -1;  // self-reducing deferred split-K (opt-in: CV_WGRAD_SELF, cv_debug_wgrad_self)
 
 static int launch_wgrad_reduce(const float* part, int split, int M, int N, int ntot, int cb, int kk, float* gw,
                                float* gbias, hipStream_t st) {
@@ -1439,6 +1444,30 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
     atomic_splits = (e && atoi(e) != 0) ? 1 : 0;
   }
   if (atomic_splits) work = nullptr;
+  // Self-reducing split (deferred gradients, opt-in CV_WGRAD_SELF=1 / cv_debug_wgrad_self): every K slice parks its
+  // fragments as a slab in `work` and takes its tile's ticket (the device's in-launch split-K tickets,
+  // cv_set_gemm_workspace); the slice that draws the last ticket sums the slabs in slice order and adds the tile into
+  // gweight / gbias itself, so no partials are left for cv_step_reduce to read back (VAE64 bs = 256: ~240 MB per
+  // step).  Measured slower (round 6, same box, two rounds): MNIST 0.4748 -> 0.6097 ms, CelebA 2.093 -> 2.269 ms,
+  // PACS 0.894 -> 0.962 ms, C5 bf16 1.213 -> 1.412 ms — the last slice of every tile sums 8-16 slabs alone, a serial
+  // tail per tile, where cv_step_reduce streams all partials at ~4.6 TB/s in one wide launch.
+  if (g_wgrad_self < 0) {
+    const char* e = getenv("CV_WGRAD_SELF");
+    g_wgrad_self = e ? (atoi(e) != 0) : 0;
+  }
+  if (w.split > 1 && work && g_wgrad_self && g_defer_sink) {
+    const long tiles = (long)cdiv(a.M, w.BM) * cdiv(Ntot, w.BN);
+    const size_t slab = (size_t)w.split * tiles * w.BM * w.BN * sizeof(float);
+    float* fpart = nullptr;
+    unsigned* cnt = nullptr;
+    size_t pbytes = 0;
+    if (tiles <= (long)FIX_CNT_WORDS && work_bytes >= slab && fix_workspace(fpart, cnt, pbytes)) {
+      a.fix_part = work;
+      a.fix_cnt = cnt;
+      if (launch(a, w.BM, w.BN, w.split, st)) return 1;
+      return 0;  // (the defer record stays split 0: nothing left to reduce)
+    }
+  }
   if (w.split > 1 && work) {
     const size_t need = (size_t)w.split * a.M * Ntot * sizeof(float);
     CV_REQUIRE(work_bytes >= need, "wgrad: workspace %zu bytes < %zu needed", work_bytes, need);
@@ -1467,6 +1496,12 @@ extern "C" int cv_set_gemm_workspace(void* work, size_t bytes) {
   g_fix_work[dev] = work;
   g_fix_bytes[dev] = work ? bytes : 0;
   return 0;
+}
+
+extern "C" int cv_debug_wgrad_self(int on) {
+  const int prev = g_wgrad_self;
+  if (on >= 0) g_wgrad_self = on ? 1 : 0;
+  return prev;
 }
 
 extern "C" int cv_debug_pm(int on) {

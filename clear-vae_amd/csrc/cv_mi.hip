@@ -965,8 +965,17 @@ extern "C" int cv_adam_step(float* params, const float* grads, float* exp_avg, f
   CV_REQUIRE(params && grads && exp_avg && exp_avg_sq && hyper && step && numel > 0, "adam_step: bad args");
   CV_REQUIRE(((uintptr_t)params | (uintptr_t)grads | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
              "adam_step: buffers must be 16-byte aligned");
+  // up to 2048 workgroups (CV_ADAM_WG): the update is HBM-bound (7 x 4 bytes per parameter) and each thread has one
+  // float4 of each operand in flight per iteration, so the bytes in flight scale with the resident waves (round 5's
+  // 512-workgroup cap held the VAE64 arena's 171 MB at ~3.8 TB/s)
+  static long cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("CV_ADAM_WG");
+    cap = e ? atol(e) : 2048;
+    if (cap < 1) cap = 2048;
+  }
   long g = (numel / 4 + 255) / 256;
-  if (g > 512) g = 512;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(adam_kernel, dim3(g), dim3(256), 0, S(stream), params, grads, exp_avg, exp_avg_sq, (long)numel,
                      hyper, step, grad_scale, aux_counter);

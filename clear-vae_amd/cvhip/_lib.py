@@ -285,6 +285,7 @@ _SIGS = {
     ),
     "cv_ntxent_aux_flush": (c_int, [c_void_p]),
     "cv_ntxent_aux_discard": (c_int, []),
+    "cv_debug_wgrad_self": (c_int, [c_int]),
     "cv_latent_combine_workspace_bytes": (c_size_t, []),
     "cv_ntxent_aux_pending": (c_int, []),
     "cv_ntxent_aux_combine": (

@@ -617,6 +617,11 @@ int cv_debug_pm(int on);
 int cv_debug_pm_count(int reset);
 /* test hook: 1 (default) lets a queued NT-Xent phase ride in a served direct launch (cv_ntxent_aux), 0 launches it
  * on its own at the flush; a negative value only queries; returns the previous setting */
+/* test hook: 1 (CV_WGRAD_SELF=1; measured slower, off by default) lets a deferred split-K weight gradient reduce its
+ * own slices (the split's last slice adds the tile into gweight; the defer record says split 0), 0 (default) leaves
+ * the partials for cv_step_reduce;
+ * -1 queries; returns the previous setting (-1: not yet read from the environment) */
+int cv_debug_wgrad_self(int on);
 int cv_debug_aux(int on);
 /* test hook: direct + NT-Xent grids issued since the last reset */
 int cv_debug_aux_count(int reset);

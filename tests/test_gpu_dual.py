@@ -52,7 +52,7 @@ def _bn(lib, C, count, rng, dev, y=None, gsum=None):
     return s, t
 
 
-def _run(name, dual):
+def _run(name, dual, self_reduce=None):
     from cvhip import _lib
 
     n, tr, cin, hin, cout, hout, k, s, p = PAIRS[name]
@@ -89,6 +89,7 @@ def _run(name, dual):
     d = _lib.cv_wgrad_defer()
     st = _lib.stream_handle()
     prev = L.cv_debug_dual(1 if dual else 0)
+    prev_self = L.cv_debug_wgrad_self(-1 if self_reduce is None else int(self_reduce))
     L.cv_debug_dual_count(1)
     try:
         _lib.call("cv_conv_backward_deferred_kpack", ctypes.byref(g), ctypes.byref(gout), Wb.data_ptr(),
@@ -98,11 +99,17 @@ def _run(name, dual):
         issued = L.cv_debug_dual_count(1)
     finally:
         L.cv_debug_dual(prev)
-    assert d.split > 0 and d.part == work.data_ptr()
-    parts = work[: d.split * d.M * d.ntot].clone()
-    _lib.call("cv_step_reduce", (_lib.cv_wgrad_defer * 1)(d), 1, None, 0, None, None, 0, ctypes.c_float(0.1), None,
-              st)
-    torch.cuda.synchronize()
+        if self_reduce is not None:
+            L.cv_debug_wgrad_self(prev_self)
+    # (two forms: the split's partials recorded for cv_step_reduce (the default), or — the opt-in self-reducing
+    # split — the split's last slice already added the gradient and the record says split 0)
+    parts = None
+    if d.split > 0:
+        assert d.part == work.data_ptr()
+        parts = work[: d.split * d.M * d.ntot].clone()
+        _lib.call("cv_step_reduce", (_lib.cv_wgrad_defer * 1)(d), 1, None, 0, None, None, 0, ctypes.c_float(0.1),
+                  None, st)
+        torch.cuda.synchronize()
     host = dict(x=x, dz=dz, yo=yo, W=W, tin=tin, tout=tout, geom=PAIRS[name])
     return dict(issued=issued, gin=gin.clone(), gsum=tin["gstat"].sum(0).cpu(), cbwd=tin["cbwd"].cpu(),
                 ticket=int(tin["ticket"][1].item()), split=(d.split, d.M, d.ntot), parts=parts, gw=gw.clone(),
@@ -148,7 +155,7 @@ def test_dual_grid_matches_back_to_back(name):
     c2 = gs_on[1] / cnt
     assert rel(on["cbwd"][cin:2 * cin], c1) < 1e-6 and rel(on["cbwd"][4 * cin:5 * cin], c2) < 1e-6
     # weight gradient: partials bit-identical when both plans coincide, reduced gradients within 2e-6 always
-    if on["split"] == off["split"]:
+    if on["split"] == off["split"] and on["parts"] is not None:
         assert torch.equal(on["parts"], off["parts"])
     assert rel(on["gw"], off["gw"]) < 2e-6, rel(on["gw"], off["gw"])
     # both against fp64
@@ -158,3 +165,17 @@ def test_dual_grid_matches_back_to_back(name):
     xh = (v - v.mean(0)) / torch.sqrt(v.var(0, unbiased=False) + 1e-5)
     want = torch.stack([gin_ref.sum(0), (gin_ref * xh).sum(0)])
     assert rel(gs_on, want) < 1e-5
+
+
+@pytest.mark.parametrize("name", list(PAIRS))
+@pytest.mark.parametrize("dual", [True, False], ids=["dual", "back-to-back"])
+def test_self_reducing_wgrad_matches_step_reduce(name, dual):
+    """The deferred weight gradient reduced by its own last slice (cv_debug_wgrad_self(1), opt-in) against the
+    same partials summed by cv_step_reduce (0): the same slabs in the same slice order, added by another kernel's
+    association — within 2e-6 — and both against fp64 at 1e-5; the data gradient is unaffected (bit-identical)."""
+    a, b = _run(name, dual, True), _run(name, dual, False)
+    assert a["split"][0] == 0 and b["split"][0] > 1, (a["split"], b["split"])
+    assert torch.equal(a["gin"], b["gin"])
+    assert rel(a["gw"], b["gw"]) < 2e-6, rel(a["gw"], b["gw"])
+    gin_ref, gw_ref, _ = _fp64(a["host"])
+    assert rel(a["gw"], gw_ref) < TOL, rel(a["gw"], gw_ref)
