@@ -131,12 +131,13 @@ __global__ __launch_bounds__(1024) void combine_kernel(const CombineArgs C) {
 // CV_COMBINE_WG=0, or no workspace: the one-workgroup kernel.
 constexpr int CMB_NT = 256;
 constexpr int CMB_MAXG = 64;
+constexpr int CMB_SLOTS = 1024;  // KL partial slots of the workspace (combine_multi: CMB_MAXG; combine_dz: dz tiles)
 __global__ __launch_bounds__(CMB_NT) void combine_multi_kernel(const CombineArgs C, double* __restrict__ work) {
   __shared__ double scratch[16];
   __shared__ int last;
   double kc, ks;
   const float w = combine_sums<CMB_NT>(C, blockIdx.x * CMB_NT * 8, gridDim.x * CMB_NT * 8, scratch, &kc, &ks);
-  unsigned* ticket = reinterpret_cast<unsigned*>(work + 2 * CMB_MAXG);
+  unsigned* ticket = reinterpret_cast<unsigned*>(work + 2 * CMB_SLOTS);
   if (threadIdx.x == 0) {
     work[2 * blockIdx.x] = kc;
     work[2 * blockIdx.x + 1] = ks;
@@ -169,6 +170,143 @@ __global__ __launch_bounds__(CMB_NT) void combine_multi_kernel(const CombineArgs
       C.losses[2] = (float)(-0.5 * b / (double)C.n);
       C.losses[7] = w;
     }
+  }
+}
+
+// The combine with the decoder-input gradient dz = d(h) W computed here, deterministically (trainer.py:452-480 through
+// the decoder Linear, vae.py:33, and z = mu + eps exp(lv / 2), vae.py:56-60).  The decoder-input backward used to add
+// dz in 16-feature partials with fp32 atomics (128 workgroups onto every element): the one order-dependent sum of the
+// fused step (round 6: with it removed, replays of the MNIST and CelebA steps from the same state are bit-identical).
+// Workgroup (s, rb, jt) contracts F / S storage columns (slice s) for dz rows 16 rb .. 16 rb + 15, columns 16 jt ..
+// 16 jt + 15 on v_mfma_f32_16x16x4_f32 (lane l: a float4 of d(h) row l % 16 at 4 (l / 16) consecutive columns, and W
+// of those columns' features at z column l % 16; step s2 contracts k = 4 (l / 16) + s2), its four waves' tiles added
+// in wave order, and parks the tile in the workspace.  The last of a tile's S slices to arrive (release / acquire
+// around the tile's ticket) adds the S tiles in slice order and runs the combine of its 256 elements (the arithmetic
+// of combine_sums); the KL partials of the tiles go to the workspace's slots, summed in tile order by the last tile
+// (combine_multi_kernel's protocol).  Every sum has a fixed order.
+constexpr int CDZ_S = 8;  // most F slices (workgroups per 16 x 16 dz tile); default 4 (CV_CDZ_S)
+__global__ __launch_bounds__(256) void combine_dz_kernel(const CombineArgs C, const float* __restrict__ gh,
+                                                         const float* __restrict__ W, int F, int pix, int ch, int S,
+                                                         float* __restrict__ dz_out, double* __restrict__ work) {
+  __shared__ float red[4][16][17];
+  __shared__ double scratch[16];
+  __shared__ int last;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int n = C.n, d = C.d, K = 2 * d;
+  const int sl = blockIdx.x, rb = blockIdx.y, jt = blockIdx.z;
+  const int ntile = gridDim.y * gridDim.z, tile = rb + gridDim.y * jt;
+  const int row_l = 16 * rb + (l & 15), q = l >> 4, jl = 16 * jt + (l & 15);
+  const bool rok = row_l < n, jok = jl < K;
+  const float* grow = gh + (size_t)(rok ? row_l : 0) * F;
+  const int per = F / S, c_beg = sl * per + w * (per >> 2), c_end = c_beg + (per >> 2);  // (host: F % (64 S) == 0)
+  // (storage column col -> PyTorch feature (col % ch) pix + col / ch; ch % 4 == 0, so the 4 columns of a float4 are
+  // features f0, f0 + pix, f0 + 2 pix, f0 + 3 pix)
+  auto feat = [&](int col) { return pix <= 1 ? col : (col % ch) * pix + col / ch; };
+  const int fstep = pix <= 1 ? 1 : pix;
+  // the combine operands of this thread's element, requested before the contraction (used by the tile's last slice)
+  const int i = t >> 4, jj = t & 15, row = 16 * rb + i, j = 16 * jt + jj;
+  const bool eok = row < n && j < K;
+  const int eblk = (j < d) ? 0 : 2, ek = (j < d) ? j : j - d;
+  const size_t hm = eok ? (size_t)row * 4 * d + eblk * d + ek : 0, hl = hm + (eok ? d : 0);
+  const float m = C.heads[hm], lv = C.heads[hl], zz = C.z[eok ? (size_t)row * K + j : 0];
+  const float om = C.accumulate ? C.dheads[hm] : 0.f, ol = C.accumulate ? C.dheads[hl] : 0.f;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;  // 16-column chunks whose loads are in flight together
+  for (int c0 = c_beg; c0 < c_end; c0 += 16 * U) {
+    f32x4 a[U];
+    float b[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = c0 + 16 * u + 4 * q;
+      const bool in = cc < c_end;
+      a[u] = *reinterpret_cast<const f32x4*>(grow + (in ? cc : c_beg));
+      const float* wp = W + (size_t)feat(in ? cc : c_beg) * K + jl;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) b[u][s2] = (jok && in) ? wp[(size_t)s2 * fstep * K] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(rok ? a[u][s2] : 0.f, b[u][s2], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[w][4 * q + r][l & 15] = acc[r];
+  __syncthreads();
+  unsigned* gticket = reinterpret_cast<unsigned*>(work + 2 * CMB_SLOTS);
+  unsigned* tticket = gticket + 2;
+  float* part = reinterpret_cast<float*>(work + 2 * CMB_SLOTS + 1 + CMB_SLOTS / 2);
+  const float mine = ((red[0][i][jj] + red[1][i][jj]) + red[2][i][jj]) + red[3][i][jj];
+  float g = mine;
+  if (S > 1) {
+    part[((size_t)tile * S + sl) * 256 + t] = mine;
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      last = __hip_atomic_fetch_add(tticket + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)S - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(tticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    if (!last) return;
+    // the tile's last slice: dz = the S slice tiles in slice order, then the combine of its 256 elements
+    float pv[CDZ_S];
+#pragma unroll
+    for (int s2 = 0; s2 < CDZ_S; ++s2)
+      pv[s2] = s2 < S ? (s2 == sl ? mine : __hip_atomic_load(part + ((size_t)tile * S + s2) * 256 + t, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)) : 0.f;
+    g = pv[0];
+#pragma unroll
+    for (int s2 = 1; s2 < CDZ_S; ++s2)
+      if (s2 < S) g += pv[s2];
+  }
+  const double tt = (double)C.anneal_step[0];
+  const float wgt = (float)((double)C.beta / (1.0 + exp(-(tt - (double)C.loc) / (double)C.scale)));
+  double sc = 0.0, ss = 0.0;
+  if (eok) {
+    if (dz_out) dz_out[(size_t)row * K + j] = g;
+    const float inv_n = 1.0f / (float)n;
+    const float el = expf(lv);
+    const double term = (double)(1.0f + lv - m * m - el);
+    if (j < d) sc = term; else ss = term;
+    const float vm = wgt * m * inv_n + g;
+    const float vl = wgt * (-0.5f * inv_n) * (1.0f - el) + g * (zz - m) * 0.5f;
+    C.dheads[hm] = C.accumulate ? om + vm : vm;
+    C.dheads[hl] = C.accumulate ? ol + vl : vl;
+  }
+  const double kc = block_sum<256>(sc, scratch);
+  const double ks = block_sum<256>(ss, scratch);
+  if (t == 0) {
+    work[2 * tile] = kc;
+    work[2 * tile + 1] = ks;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = __hip_atomic_fetch_add(gticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ntile - 1;
+  }
+  __syncthreads();
+  if (!last || t >= 64) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double a = 0.0, bsum = 0.0;  // (lane t sums slots t, t + 64, ... in order; then a fixed shuffle tree)
+  for (int s2 = t; s2 < ntile; s2 += 64) {
+    a += __hip_atomic_load(work + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bsum += __hip_atomic_load(work + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64);
+    bsum += __shfl_down(bsum, o, 64);
+  }
+  if (t == 0) {
+    __hip_atomic_store(gticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (C.rec_in) {
+      double r = 0.0;
+      for (int q2 = 0; q2 < CV_REC_REPL; ++q2) r += C.rec_in[q2];
+      C.losses[0] = (float)r;
+    }
+    C.losses[1] = (float)(-0.5 * a / (double)n);
+    C.losses[2] = (float)(-0.5 * bsum / (double)n);
+    C.losses[7] = wgt;
   }
 }
 
@@ -761,7 +899,14 @@ extern "C" int cv_kl(const float* mu, const float* logvar, int ld, int n, int d,
   return 0;
 }
 
-extern "C" size_t cv_latent_combine_workspace_bytes(void) { return (2 * CMB_MAXG + 1) * sizeof(double); }
+extern "C" size_t cv_latent_combine_workspace_bytes(void) { return (2 * CMB_SLOTS + 1) * sizeof(double); }
+
+// cv_latent_combine_dz's workspace: the KL slots, the tickets and the slice tiles of the dz contraction
+extern "C" size_t cv_latent_combine_dz_workspace_bytes(int n, int d) {
+  if (n <= 0 || d <= 0) return 0;
+  const size_t tiles = (size_t)cdiv(n, 16) * cdiv(2 * d, 16);
+  return (2 * CMB_SLOTS + 1 + CMB_SLOTS / 2) * sizeof(double) + tiles * CDZ_S * 256 * sizeof(float);
+}
 
 extern "C" int cv_latent_combine(const float* heads, const float* z, const float* dz, int n, int d, float beta,
                                  float loc, float scale, const int64_t* anneal_step, const double* rec_in,
@@ -782,6 +927,40 @@ extern "C" int cv_latent_combine_acc(const float* heads, const float* z, const f
   const CombineArgs C{heads, z, dz, n, d, beta, loc, scale, anneal_step, rec_in, dheads, losses, 1};
   combine_launch(C, work, S(stream));
   CV_LAUNCH_CHECK("latent_combine_acc");
+  return 0;
+}
+
+extern "C" int cv_latent_combine_dz(const float* heads, const float* z, const float* dh, const float* weight,
+                                    const cv_linear* lin, float beta, float loc, float scale,
+                                    const int64_t* anneal_step, const double* rec_in, float* dheads, float* losses,
+                                    float* dz_out, int accumulate, double* work, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(heads && z && dh && weight && lin && anneal_step && dheads && losses && work,
+             "latent_combine_dz: null args");
+  const int n = lin->n, K = lin->in_features, F = lin->out_features;
+  CV_REQUIRE(n > 0 && K > 0 && K % 2 == 0 && F > 0 && F % 64 == 0, "latent_combine_dz: n=%d K=%d F=%d (F %% 64 == 0)",
+             n, K, F);
+  const int pix = lin->out_pix > 0 ? lin->out_pix : 1, ch = lin->out_ch;
+  CV_REQUIRE(pix <= 1 || pix * ch == F, "latent_combine_dz: out_pix*out_ch != out_features");
+  CV_REQUIRE(((uintptr_t)dh & 15) == 0, "latent_combine_dz: d(h) must be 16-byte aligned");
+  static int ns0 = -1;  // F slices (CV_CDZ_S A/B: 1, 2, 4, 8)
+  if (ns0 < 0) {
+    const char* e = getenv("CV_CDZ_S");
+    // (MNIST, same box, two rounds: 1 / 2 / 4 / 8 slices 0.4801 / 0.4779 / 0.4774 / 0.4801 ms against 0.4753 with the
+    // atomic dz partials: determinism costs ~2 us there)
+    ns0 = e ? atoi(e) : 4;
+    if (ns0 < 1 || ns0 > CDZ_S) ns0 = CDZ_S;
+  }
+  int ns = ns0;
+  while (ns > 1 && F % (64 * ns)) ns >>= 1;  // (F / ns: a multiple of 4 waves x 16 columns)
+  CV_REQUIRE(pix <= 1 || ch % 4 == 0, "latent_combine_dz: out_ch %% 4 != 0");
+  const dim3 grid((unsigned)ns, (unsigned)cdiv(n, 16), (unsigned)cdiv(K, 16));
+  CV_REQUIRE((long)grid.y * grid.z <= CMB_SLOTS, "latent_combine_dz: %ld dz tiles > %d slots", (long)grid.y * grid.z,
+             CMB_SLOTS);
+  const CombineArgs C{heads, z, nullptr, n, K / 2, beta, loc, scale, anneal_step, rec_in, dheads, losses, accumulate};
+  note_launch((const void*)combine_dz_kernel);
+  hipLaunchKernelGGL(combine_dz_kernel, grid, dim3(256), 0, S(stream), C, dh, weight, F, pix, ch, ns, dz_out, work);
+  CV_LAUNCH_CHECK("latent_combine_dz");
   return 0;
 }
 

@@ -287,6 +287,12 @@ _SIGS = {
     "cv_ntxent_aux_discard": (c_int, []),
     "cv_debug_wgrad_self": (c_int, [c_int]),
     "cv_latent_combine_workspace_bytes": (c_size_t, []),
+    "cv_latent_combine_dz_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "cv_latent_combine_dz": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, _P(cv_linear), c_float, c_float, c_float, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    ),
     "cv_ntxent_aux_pending": (c_int, []),
     "cv_ntxent_aux_combine": (
         c_int,

@@ -109,6 +109,12 @@ LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 # grids 6 + 4 us (0.4735 -> 0.4820 ms with them there: CVHIP_LATENT_AUX_DL=2 forces it).
 LATENT_AUX_DL = int(os.environ.get("CVHIP_LATENT_AUX_DL", "1"))
 
+# CVHIP_DET_DZ (default 1; the LATENT_AUX / LATENT_SIDE schedules): the decoder-input gradient dz = d(h) W is computed
+# by the latent combine launch (cv_latent_combine_dz, fixed-order sums) instead of as fp32-atomic partials in the
+# decoder-input backward — the fused step's only order-dependent sum, so with it replays from the same state are
+# bit-identical (tests/test_gpu_determinism.py); 0: the atomic partials (A/B)
+DET_DZ = os.environ.get("CVHIP_DET_DZ", "1") == "1"
+
 # CVHIP_MIM_BRANCHES (default 2; 0: the sequential form): CLEAR-MIM's five estimator-update decoder forwards
 # (trainer.py:873-888) on this many side lanes of the single-GPU step graph, beside the five estimator learning steps
 # on the step's stream (ClearStep._programs, make_learn_branched).  Measured (round 6, VAE64 n = 256, the five
@@ -467,8 +473,9 @@ class ClearStep:
         dp = self.dp
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
         dec = Program()
+        det_dz = DET_DZ and (side_nt or aux_nt) and not chain_nt and ws.fused_decoder_input()
         ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer,
-                                    aux_in=aux_args[1] if dl_nt else None)
+                                    aux_in=aux_args[1] if dl_nt else None, dz_later=det_dz)
         if dl_nt:
             dec.keep.append(br_arr)
         if dp:
@@ -488,9 +495,15 @@ class ClearStep:
             # (side stream: join it first) the KL + decoder-chain seed added onto the NT-Xent gradients
             if side_nt:
                 lat.add_join()
-            lat.add("cv_latent_combine_acc", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
-                    ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))), self.anneal,
-                    ws.rec, ws.dheads, ws.losses, ws.comb_work)
+            if det_dz:  # (dz = d(h) W here, in fixed order, written to ws.dz for any later reader)
+                lat.add("cv_latent_combine_dz", ws.heads, ws.z, ws.gah, sp.dec_lin.weight, ws.decoder_input_geometry(),
+                        ctypes.c_float(float(hp["beta"])), ctypes.c_float(float(hp.get("loc", 0))),
+                        ctypes.c_float(float(hp.get("scale", 1))), self.anneal, ws.rec, ws.dheads, ws.losses, ws.dz,
+                        1, ws.comb_dz_work)
+            else:
+                lat.add("cv_latent_combine_acc", ws.heads, ws.z, ws.dz, n, d, ctypes.c_float(float(hp["beta"])),
+                        ctypes.c_float(float(hp.get("loc", 0))), ctypes.c_float(float(hp.get("scale", 1))),
+                        self.anneal, ws.rec, ws.dheads, ws.losses, ws.comb_work)
             lat_inj = Program()
             lat_inj.extend(lat)
         if branches is not None and not side_nt and not aux_nt:

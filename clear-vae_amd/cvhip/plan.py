@@ -672,6 +672,9 @@ class Workspace:
             # the multi-workgroup latent combine's KL partial slots + arrival ticket (zeroed once; left zeroed)
             self.comb_work = torch.zeros(int(_lib.lib().cv_latent_combine_workspace_bytes()) // 8 + 1,
                                          dtype=torch.float64, device=f32["device"])
+            # cv_latent_combine_dz: KL slots, tickets and the dz contraction's slice tiles (zeroed once)
+            self.comb_dz_work = torch.zeros(int(_lib.lib().cv_latent_combine_dz_workspace_bytes(n, d)) // 8 + 1,
+                                            dtype=torch.float64, device=f32["device"])
             self.mi_work = torch.zeros(int(_lib.lib().cv_mi_workspace_bytes(n)) // 4 + 16, **f32)
             # split-K partial tiles of the weight-gradient GEMMs (one launch at a time on the stream)
             L = _lib.lib()
@@ -830,6 +833,11 @@ class Workspace:
     # launch first (measured: 26.4 us for the drawing launch vs ~5 + 11.7 us)
     DECIN_DRAW = os.environ.get("CVHIP_DECIN_DRAW", "0") == "1"
 
+    def decoder_input_geometry(self):
+        sp = self.spec
+        Cu, Hu, Wu = sp.unflat
+        return cv_linear(self.n, 2 * sp.d, sp.dec_lin.out_features, 1, 0, Hu * Wu, Cu, LIN_MMA)
+
     def fused_decoder_input(self) -> bool:
         sp = self.spec
         return self.FUSED_DECIN and bool(_lib.lib().cv_decoder_input_supported(self.n, sp.d, sp.dec_lin.out_features))
@@ -916,10 +924,12 @@ class Workspace:
             P.add("cv_output_forward", self.bn_dec[-1].cv(train), cur, n, sp.in_ch, hw, self.xhat)
 
     def decoder_backward_program(self, P: Program, param_grad, dz_out, zero_dz: bool = True, defer=None,
-                                 aux_in=None):
+                                 aux_in=None, dz_later: bool = False):
         """From dv (= self.g_dec[-1], masked grad at the output BN, with its gstat filled) down to
         dz_out [n, 2d] (zeroed + accumulated) and the decoder parameter gradients.  aux_in: cv_ntxent_aux arguments
-        queued before the decoder-input backward launch (which serves it) and flushed after it."""
+        queued before the decoder-input backward launch (which serves it) and flushed after it.  dz_later: the fused
+        decoder-input backward leaves dz to the latent combine (cv_latent_combine_dz: deterministic) and writes only
+        d(h) into gah."""
         sp, n = self.spec, self.n
         L = len(sp.dec)
         for li in range(L - 1, -1, -1):
@@ -944,7 +954,7 @@ class Workspace:
             if aux_in is not None:
                 P.add("cv_ntxent_aux", *aux_in)
             P.add("cv_decoder_input_backward", lin, self.gah, self.h, self.bn_1d.cv(True), self.bn_1d.gstat,
-                  self.z, param_grad(sp.dec_lin.weight), sp.dec_lin.weight, dz_out)
+                  self.z, param_grad(sp.dec_lin.weight), sp.dec_lin.weight, None if dz_later else dz_out)
             if aux_in is not None:
                 P.add("cv_ntxent_aux_flush")
             return

@@ -381,6 +381,16 @@ int cv_latent_combine_acc(const float* heads, const float* z, const float* dz, i
  * arrival order); NULL runs the one-workgroup kernel.  Two launches that may overlap in time (two streams) need two
  * workspaces. */
 size_t cv_latent_combine_workspace_bytes(void);
+/* cv_latent_combine(_acc) (accumulate 0 / 1) with the decoder-input gradient computed here: dz = d(h) W, d(h) the
+ * decoder Linear's output gradient [n][F] in storage order (cv_decoder_input_backward's `ga` after the call, with
+ * dz = NULL there), W the Linear weight [F][2d] (lin: the decoder Linear's geometry, out_pix / out_ch its Unflatten;
+ * F % 64 == 0).  Deterministic: every dz element is one fixed-order sum (the atomics of the decoder-input backward's
+ * dz partials were the fused step's only order-dependent sum).  dz_out (or NULL) receives dz.  work (required): a
+ * caller-owned device workspace of cv_latent_combine_dz_workspace_bytes(n, d), zeroed once before its first use. */
+size_t cv_latent_combine_dz_workspace_bytes(int n, int d);
+int cv_latent_combine_dz(const float* heads, const float* z, const float* dh, const float* weight, const cv_linear* lin,
+                         float beta, float loc, float scale, const int64_t* anneal_step, const double* rec_in,
+                         float* dheads, float* losses, float* dz_out, int accumulate, double* work, cv_stream_t stream);
 
 /* reconstruction term (losses.py:45-47) for the autograd path: rec = mean_n sum (xhat - x)^2;
  * work: one zeroed fp64 word.  dxhat != NULL: dxhat = gscale[0] * 2 (xhat - x) / n. */
