@@ -664,7 +664,79 @@ struct PackArgs {
   int cn;
   // flat 1-D grid: workgroups [wg0[l], wg0[l + 1]) pack layer l, the workgroups from wg0[n] on zero / copy
   int wg0[MAX_PACK + 1];
+  // Adam fused in (cv_adam_pack_step; ad == 0: off): the packing workgroups update their tile's parameters (p, m,
+  // v at the arena offset of src) before packing the new values; the slice workgroups update the arena ranges no
+  // item covers (plain); the last workgroup to finish advances the step counters
+  int ad;
+  float* ap;
+  const float* ag;
+  float* am;
+  float* av;
+  const float* hyper;
+  int64_t* step;
+  const float* gscale;
+  int64_t* aux;
+  long plain0[2 * MAX_PACK + 2];
+  long plainn[2 * MAX_PACK + 2];
+  int nplain;
 };
+
+// Adam constants of the step (the arithmetic of adam_kernel, cv_mi.hip); computed by thread 0 into sh[8]
+__device__ __forceinline__ void adam_consts(const PackArgs& a, float* sh) {
+  if (threadIdx.x == 0) {
+    const long t_step = a.step[0] + 1;
+    const double b1 = a.hyper[1], b2 = a.hyper[2];
+    const double bc1 = 1.0 - pow(b1, (double)t_step);
+    const double bc2 = 1.0 - pow(b2, (double)t_step);
+    sh[0] = (float)(-(double)a.hyper[0] / bc1);
+    sh[1] = (float)sqrt(bc2);
+    sh[2] = (float)(1.0 - b1);
+    sh[3] = (float)(1.0 - b2);
+    sh[4] = a.hyper[2];
+    sh[5] = a.hyper[3];
+    sh[6] = a.hyper[4];
+    sh[7] = a.gscale ? a.gscale[0] : 1.0f;
+  }
+}
+// torch.optim.Adam on one element (adam_kernel's upd): returns the new parameter, updates mm / vv
+__device__ __forceinline__ float adam_upd(const float* c, float g, float pp, float& mm, float& vv) {
+  g *= c[7];
+  if (c[6] != 0.f) g = g + c[6] * pp;
+  mm = mm + c[2] * (g - mm);
+  vv = vv * c[4] + c[3] * g * g;
+  const float den = sqrtf(vv) / c[1] + c[5];
+  return pp + c[0] * (mm / den);
+}
+// the step counters: every workgroup of an Adam launch arrives once; the last advances step[0] (and aux)
+__device__ __forceinline__ void adam_arrive(const PackArgs& a, int* flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long prev = atomicAdd((unsigned long long*)(a.step + 1), 1ull);
+    *flag = prev == (unsigned long long)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (*flag && threadIdx.x == 0) {
+    a.step[0] += 1;
+    a.step[1] = 0;
+    if (a.aux) a.aux[0] += 1;
+  }
+}
+// the slice workgroups of an Adam launch: the arena ranges no packed item covers
+__device__ __forceinline__ void adam_plain_slice(const PackArgs& a, const float* c, const long b, const long nb) {
+  long tot = 0;
+  for (int r = 0; r < a.nplain; ++r) tot += a.plainn[r];
+  for (long i = b * 256 + threadIdx.x; i < tot; i += nb * 256) {
+    int r = 0;
+    long o = i;
+    while (r + 1 < a.nplain && o >= a.plainn[r]) o -= a.plainn[r++];
+    const long e = a.plain0[r] + o;
+    float mm = a.am[e], vv = a.av[e];
+    const float np = adam_upd(c, a.ag[e], a.ap[e], mm, vv);
+    a.am[e] = mm;
+    a.av[e] = vv;
+    a.ap[e] = np;
+  }
+}
 // the layer of flat workgroup v (wg0 prefix sums; v >= wg0[n]: the zero / copy slice, returns n)
 __device__ __forceinline__ int pack_layer_of(const PackArgs& a, int v) {
   int l = 0;
@@ -690,9 +762,20 @@ __device__ __forceinline__ void pack_zero_slice(const PackArgs& a, const long b,
 }
 // small layers: one destination element per thread, each destination walked in its own order
 __global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
+  __shared__ float ac[8];
+  __shared__ int flag;
   const int v = blockIdx.x, l = pack_layer_of(a, v);
+  if (a.ad) {
+    adam_consts(a, ac);
+    __syncthreads();
+  }
   if (l == a.n) {
-    pack_zero_slice(a, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
+    if (a.ad) {
+      adam_plain_slice(a, ac, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
+      adam_arrive(a, &flag);
+    } else {
+      pack_zero_slice(a, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
+    }
     return;
   }
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
@@ -700,6 +783,23 @@ __global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
   const float* __restrict__ src = a.src[l];
   const FDiv f_cs = FDiv::make(cs), f_cb = FDiv::make(cbn);
   const int b = v - a.wg0[l], nb = a.wg0[l + 1] - a.wg0[l];
+  if (a.ad) {  // one source element per thread: Adam, then its two packed positions
+    const long o0 = src - a.ap;
+    const FDiv f_kk = FDiv::make(kk);
+    for (int e = b * 256 + threadIdx.x; e < total; e += nb * 256) {
+      const long o = o0 + e;
+      float mm = a.am[o], vv = a.av[o];
+      const float np = adam_upd(ac, a.ag[o], a.ap[o], mm, vv);
+      a.am[o] = mm;
+      a.av[o] = vv;
+      a.ap[o] = np;
+      const int q = f_kk.div(e), tap = e - q * kk, c_s = f_cb.div(q), c_b = q - c_s * cbn;
+      if (a.dg[l]) a.dg[l][(tap * cbn + c_b) * cs + c_s] = np;
+      if (a.ds[l]) a.ds[l][(tap * cs + c_s) * cbn + c_b] = np;
+    }
+    adam_arrive(a, &flag);
+    return;
+  }
   for (int j = b * 256 + threadIdx.x; j < total; j += nb * 256) {
     if (a.dg[l]) {  // [tap][cb][cs]
       const int q = f_cs.div(j), c_s = j - q * cs, tap = f_cb.div(q), c_b = q - tap * cbn;
@@ -718,11 +818,23 @@ __global__ __launch_bounds__(256) void pack_small_kernel(const PackArgs a) {
 constexpr int PK_CS = 16, PK_CB = 32, PK_MAXK = 16;
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
   __shared__ float tile[PK_CS * PK_CB * (PK_MAXK + 1)];
+  __shared__ float ac[8];
+  __shared__ int flag;
   const int v = blockIdx.x, l = pack_layer_of(a, v);
+  if (a.ad) {
+    adam_consts(a, ac);
+    __syncthreads();
+  }
   if (l == a.n) {
-    pack_zero_slice(a, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
+    if (a.ad) {
+      adam_plain_slice(a, ac, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
+      adam_arrive(a, &flag);
+    } else {
+      pack_zero_slice(a, v - a.wg0[l], (long)gridDim.x - a.wg0[l]);
+    }
     return;
   }
+  const long ao0 = a.ad ? a.src[l] - a.ap : 0;  // (the item's arena offset: Adam's g / m / v at the same place)
   const int cs = a.cs[l], cbn = a.cb[l], kk = a.kk[l];
   const int tcb = (cbn + PK_CB - 1) / PK_CB;
   const int ntile = ((cs + PK_CS - 1) / PK_CS) * tcb;
@@ -740,11 +852,37 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
     const int tot = ncs * run;
     for (int e0 = threadIdx.x; e0 < tot; e0 += 256 * PU) {
       float v[PU];
+      if (a.ad) {  // Adam on the tile's elements (every load of the batch first), the new values packed below
+        float g[PU], m[PU], w[PU];
 #pragma unroll
-      for (int u = 0; u < PU; ++u) {
-        const int e = e0 + u * 256;
-        const int i = f_run.div(e), r = e - i * run;
-        v[u] = e < tot ? src[((size_t)(cs0 + i) * cbn + cb0) * kk + r] : 0.f;
+        for (int u = 0; u < PU; ++u) {
+          const int e = e0 + u * 256;
+          const int i = f_run.div(e), r = e - i * run;
+          const long o = ao0 + (e < tot ? ((long)(cs0 + i) * cbn + cb0) * kk + r : 0);
+          v[u] = a.ap[o];
+          g[u] = a.ag[o];
+          m[u] = a.am[o];
+          w[u] = a.av[o];
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+          const int e = e0 + u * 256;
+          const int i = f_run.div(e), r = e - i * run;
+          const long o = ao0 + ((long)(cs0 + i) * cbn + cb0) * kk + r;
+          if (e < tot) {
+            v[u] = adam_upd(ac, g[u], v[u], m[u], w[u]);
+            a.am[o] = m[u];
+            a.av[o] = w[u];
+            a.ap[o] = v[u];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+          const int e = e0 + u * 256;
+          const int i = f_run.div(e), r = e - i * run;
+          v[u] = e < tot ? src[((size_t)(cs0 + i) * cbn + cb0) * kk + r] : 0.f;
+        }
       }
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
@@ -767,6 +905,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
       }
     __syncthreads();
   }
+  if (a.ad) adam_arrive(a, &flag);
 }
 
 // ------------------------------------------------------------------ split-K reduction of WGRAD
@@ -1528,12 +1667,20 @@ CV_STAMPS_SETTER(cv_debug_set_stamps)
 
 static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, const size_t* zbytes, int zcount,
                        cv_stream_t stream, void* const* cdst = nullptr, const void* const* csrc = nullptr,
-                       const size_t* cbytes = nullptr, int ccount = 0) {
-  CV_REQUIRE(items && n > 0 && n <= MAX_PACK, "pack_conv_weights: 1..%d items", MAX_PACK);
+                       const size_t* cbytes = nullptr, int ccount = 0, const PackArgs* adam = nullptr) {
+  CV_REQUIRE((items || n == 0) && n >= 0 && n <= MAX_PACK && (n > 0 || zcount > 0 || ccount > 0),
+             "pack_conv_weights: 0..%d items (0 only with buffers to zero or copy)", MAX_PACK);
   CV_REQUIRE(zcount >= 0 && zcount <= 8 && (!zcount || (zptrs && zbytes)), "pack_conv_weights: 0..8 zeroed buffers");
   CV_REQUIRE(ccount >= 0 && ccount <= 4 && (!ccount || (cdst && csrc && cbytes)), "pack_conv_weights: 0..4 copies");
   PackArgs a;
   memset(&a, 0, sizeof(a));
+  if (adam) {  // (the Adam block: fields from ad on)
+    a.ad = 1;
+    a.ap = adam->ap; a.ag = adam->ag; a.am = adam->am; a.av = adam->av;
+    a.hyper = adam->hyper; a.step = adam->step; a.gscale = adam->gscale; a.aux = adam->aux;
+    a.nplain = adam->nplain;
+    for (int i = 0; i < adam->nplain; ++i) { a.plain0[i] = adam->plain0[i]; a.plainn[i] = adam->plainn[i]; }
+  }
   a.cn = ccount;
   for (int i = 0; i < ccount; ++i) {
     CV_REQUIRE(cdst[i] && csrc[i] && cbytes[i] % 16 == 0 && (((uintptr_t)cdst[i] | (uintptr_t)csrc[i]) & 15) == 0,
@@ -1587,6 +1734,13 @@ static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, con
     if (zg < 1) zg = 1;
     if (zg > 1024) zg = 1024;
   }
+  if (a.ad) {  // (Adam: the slice updates the plain ranges, ~4 elements per thread)
+    long tot = 0;
+    for (int r = 0; r < a.nplain; ++r) tot += a.plainn[r];
+    zg = (tot + 1023) / 1024;
+    if (zg < 1) zg = 1;
+    if (zg > 1024) zg = 1024;
+  }
   const dim3 grid((unsigned)(a.wg0[n] + zg));
   if (tiled) hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, S(stream), a);
   else hipLaunchKernelGGL(pack_small_kernel, grid, dim3(256), 0, S(stream), a);
@@ -1603,6 +1757,42 @@ extern "C" int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void*
                                          const size_t* zero_bytes, int zero_count, cv_stream_t stream) {
   clear_error();
   return pack_launch(items, n, zero_ptrs, zero_bytes, zero_count, stream);
+}
+
+extern "C" int cv_adam_pack_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                                 int64_t numel, const float* hyper, int64_t* step, const float* grad_scale,
+                                 int64_t* aux_counter, const cv_conv_pack* items, int n, cv_stream_t stream) {
+  clear_error();
+  CV_REQUIRE(params && grads && exp_avg && exp_avg_sq && hyper && step && numel > 0 && items && n > 0 &&
+                 n <= MAX_PACK, "adam_pack_step: bad args");
+  // the items' parameter ranges inside the arena, sorted: the plain ranges are the gaps
+  long lo[MAX_PACK], hi[MAX_PACK];
+  int ord[MAX_PACK];
+  for (int i = 0; i < n; ++i) {
+    const cv_conv_pack& it = items[i];
+    const long o = it.src - params, len = (long)it.cs * it.cb * it.kh * it.kw;
+    CV_REQUIRE(it.src >= params && o + len <= numel, "adam_pack_step: item %d outside the parameter arena", i);
+    lo[i] = o;
+    hi[i] = o + len;
+    ord[i] = i;
+  }
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      if (lo[ord[j]] < lo[ord[i]]) { const int q = ord[i]; ord[i] = ord[j]; ord[j] = q; }
+  PackArgs ad;
+  memset(&ad, 0, sizeof(ad));
+  ad.ap = params; ad.ag = grads; ad.am = exp_avg; ad.av = exp_avg_sq;
+  ad.hyper = hyper; ad.step = step; ad.gscale = grad_scale; ad.aux = aux_counter;
+  long cur = 0;
+  for (int k = 0; k < n; ++k) {
+    const int i = ord[k];
+    CV_REQUIRE(lo[i] >= cur, "adam_pack_step: items %d overlap", i);
+    if (lo[i] > cur) { ad.plain0[ad.nplain] = cur; ad.plainn[ad.nplain] = lo[i] - cur; ++ad.nplain; }
+    cur = hi[i];
+  }
+  if (numel > cur) { ad.plain0[ad.nplain] = cur; ad.plainn[ad.nplain] = numel - cur; ++ad.nplain; }
+  if (!ad.nplain) { ad.plain0[0] = 0; ad.plainn[0] = 0; ad.nplain = 1; }
+  return pack_launch(items, n, nullptr, nullptr, 0, stream, nullptr, nullptr, nullptr, 0, &ad);
 }
 
 extern "C" int cv_pack_conv_weights_zero_copy(const cv_conv_pack* items, int n, void* const* zero_ptrs,

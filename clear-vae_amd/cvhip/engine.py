@@ -45,7 +45,9 @@ from . import dist as cvdist
 from ._lib import (GROUP, MI_CLUBSAMPLE, MI_L1OUT, SIM, cv_latent_chain, cv_mlp, cv_mlp_grad, cv_ntxent_branch,
                    cv_tc_disc, cv_tc_grad)
 from .autograd import est_params, mlp_struct
-from .plan import DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array
+from ._lib import cv_conv_pack
+from .plan import (DeferGroup, ParamArena, Program, Workspace, ensure_arena, pack_program, ptr_array,
+                   struct_array)
 
 
 # CVHIP_FUSED_ADAM=1: single-process steps run the optimizer inside the end-of-backward reduction
@@ -108,6 +110,15 @@ LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 # grids); on MNIST (d = 8) the ConvTranspose2d placement stays: there the phases cost ~2 us each, in the decoder-input
 # grids 6 + 4 us (0.4735 -> 0.4820 ms with them there: CVHIP_LATENT_AUX_DL=2 forces it).
 LATENT_AUX_DL = int(os.environ.get("CVHIP_LATENT_AUX_DL", "1"))
+
+# CVHIP_ADAM_PACK (default 1; single GPU and data parallel, not with CVHIP_FUSED_ADAM): the VAE's Adam step packs the
+# conv weights it has just updated in the same launch (cv_adam_pack_step), so the packed copies are current when the
+# next forward starts: a replayed step's first launch only zeroes (and copies the batch), and CLEAR-MIM's / CLEAR-TC's
+# estimator forwards after the update need no packing launch.  Parameters changed outside the engine between steps
+# (load_state_dict, torch optimizers, writes into the arena buffer: anything that bumps a parameter's or the arena's
+# version counter) are repacked before the next replay; changes through a parameter's `.data` alias bypass the
+# counters: call ClearStep.invalidate_packed() after them.
+ADAM_PACK = os.environ.get("CVHIP_ADAM_PACK", "1") == "1"
 
 # CVHIP_DET_DZ (default 1; the LATENT_AUX / LATENT_SIDE schedules): the decoder-input gradient dz = d(h) W is computed
 # by the latent combine launch (cv_latent_combine_dz, fixed-order sums) instead of as fp32-atomic partials in the
@@ -277,6 +288,10 @@ class ClearStep:
         self.dp = self.world > 1 or (os.environ.get("CVHIP_FORCE_DP", "0") == "1" and dist.is_available()
                                      and dist.is_initialized())
         self.capture_collectives = GRAPH_COLLECTIVES and self.dp
+        # the VAE's Adam launch also packs the conv weights (ADAM_PACK); _packed_sig: the parameters' version
+        # counters when the packed copies were last made current (None: unknown, pack before the next replay)
+        self.adam_pack = ADAM_PACK and not (FUSED_ADAM and not self.dp)
+        self._packed_sig = None
         if self.world > 1:  # a noise stream per rank (the shards are different samples; equal noise would tie them)
             self.seed = (self.seed ^ (0x9E3779B97F4A7C15 * cvdist.rank())) & 0xFFFFFFFFFFFFFFFF
         self.gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
@@ -471,6 +486,7 @@ class ClearStep:
         # cv_step_reduce launch at the end of the backward (data parallel: one per gradient bucket, before
         # the bucket's all-reduce)
         dp = self.dp
+        adam_pack = self.adam_pack
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
         dec = Program()
         det_dz = DET_DZ and (side_nt or aux_nt) and not chain_nt and ws.fused_decoder_input()
@@ -551,13 +567,19 @@ class ClearStep:
         else:
             ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, chain=chain)
         upd = Program()
+        items = sp.pack_items["enc"] + sp.pack_items["dec"]
+        pack_arr = struct_array(cv_conv_pack, items)
+        adam_name = "cv_adam_pack_step" if adam_pack else "cv_adam_step"
+        adam_tail = (pack_arr, len(items)) if adam_pack else ()
         if dp:
-            upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
-                    self.adam.step, self.gscale, self.anneal)
+            upd.add(adam_name, A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
+                    self.adam.step, self.gscale, self.anneal, *adam_tail)
         elif not FUSED_ADAM:
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
-            upd.add("cv_adam_step", A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
-                    self.adam.step, None, self.anneal)
+            upd.add(adam_name, A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
+                    self.adam.step, None, self.anneal, *adam_tail)
+        if adam_pack:
+            upd.keep.append(pack_arr)
         else:  # single process: the optimizer step rides in the end-of-backward reduction launch
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True,
                                    adam=(A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
@@ -589,7 +611,8 @@ class ClearStep:
 
             def make_learn(inject: bool):
                 lp = Program()
-                pack_program(sp, lp, "all", zero=stats_zero)  # the VAE Adam step just moved the weights
+                # the VAE Adam step just moved the weights (ADAM_PACK: and packed them)
+                pack_program(sp, lp, None if adam_pack else "all", zero=stats_zero)
                 for j in range(5):
                     ws.decoder_program(lp, ws.z, True, "none", reparam=learn_forward(lp, j, inject))
                     ws.running_program(lp, "all")
@@ -617,7 +640,7 @@ class ClearStep:
             def make_learn_branched(inject: bool):
                 lp = Program()
                 # the VAE Adam step just moved the weights; the same launch zeroes every update's statistics
-                pack_program(sp, lp, "all", zero=[(w.stats, w.stats.numel() * 8) for w in bws])
+                pack_program(sp, lp, None if adam_pack else "all", zero=[(w.stats, w.stats.numel() * 8) for w in bws])
                 rp = (eps_buf[1] if inject else None, self.seed, self.offset)
                 zs = [ws.z] + [w.z for w in bws[1:]]
                 if not ws.encoder_program(lp, X, True, reparam=rp):  # (z_0 drawn by the heads launch, or here)
@@ -663,7 +686,7 @@ class ClearStep:
                 for j in range(5):
                     gp = Program()
                     if j == 0:
-                        pack_program(sp, gp, "all", zero=stats_zero)
+                        pack_program(sp, gp, None if adam_pack else "all", zero=stats_zero)
                     ws.decoder_program(gp, ws.z, True, "none", reparam=learn_forward(gp, j, inject))
                     ws.running_program(gp, "all")
                     gp.add("cv_mi_learning_step", mlp, zp, 2 * d, zp + 4 * d, 2 * d, n, ws.mi_work,
@@ -690,7 +713,7 @@ class ClearStep:
                 # discriminator's BCE gradients and its Adam step (data parallel: all-reduce in between)
                 gp = Program()
                 # the VAE Adam step just moved the weights; the same launch zeroes the forward's statistics
-                pack_program(sp, gp, "all", zero=[(ws.stats, ws.stats.numel() * 8)])
+                pack_program(sp, gp, None if adam_pack else "all", zero=[(ws.stats, ws.stats.numel() * 8)])
                 rp = (eps_buf[1] if inject else None, self.seed, self.offset)
                 drew = ws.encoder_program(gp, X, True, reparam=rp)
                 ws.decoder_program(gp, ws.z, True, "none", reparam=None if drew else rp)
@@ -874,6 +897,10 @@ class ClearStep:
         its own when the batch needs a conversion."""
         lab = label.reshape(-1)
         name, fn, args, _ = G["pack_call"]
+        if self.adam_pack:
+            if self._packed_sig != self._param_sig():  # (parameters changed outside the engine: repack first)
+                _lib.call("cv_pack_conv_weights", args[0], args[1], _lib.stream_handle())
+            args = (None, 0) + tuple(args[2:])  # (the packed copies are current: zero / copy only)
         nbx, nbl = G["X"].numel() * 4, G["lab"].numel() * 8
         # (folded in for small batches only: the pack launch's workgroups hold a 35 KB LDS tile each, so a large copy
         # — VAE64 bs = 256: 12.6 MB — runs slower inside it than as its own launch: CelebA +3 us, MNIST -3 us, measured)
@@ -890,6 +917,19 @@ class ClearStep:
         rc = fn(*args, _lib.stream_handle())
         if rc != 0:
             _lib.check(rc, name)
+
+    def _param_sig(self):
+        # (the parameters' own counters — load_state_dict, torch optimizers — and the arena's: writes into the flat
+        # buffer or its views; only `.data` aliases escape both)
+        sig = (self.arena.flat._version,) + tuple(p._version for p in self.arena.params)
+        if self.two_nets:
+            sig += (self.est_arena.flat._version,) + tuple(p._version for p in self.est_arena.params)
+        return sig
+
+    def invalidate_packed(self):
+        """Repack the conv weights before the next replayed step (after parameters were changed through `.data`,
+        which the version counters ADAM_PACK watches do not see)."""
+        self._packed_sig = None
 
     def step(self, X, label, before_update=None):
         """One training step on the batch (X, label).  before_update: an optional callable run (on the host, in
@@ -924,6 +964,8 @@ class ClearStep:
         else:
             self._run_eager(G, inject, before_update)
         G["count"] += 1
+        if self.adam_pack:  # (the step's Adam launch packed the weights it updated)
+            self._packed_sig = self._param_sig()
         self.steps_since_sync += 1
         self.anneal_expected += 1
         ws = G["ws"]

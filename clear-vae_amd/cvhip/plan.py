@@ -301,8 +301,9 @@ def attach_packed(spec: VaeSpec, device):
 
 def pack_program(spec: VaeSpec, P: "Program", which: str = "all", zero=None):
     """Refresh the packed conv weights from the (arena) parameters: one launch; `zero` = [(tensor,
-    bytes)] buffers cleared by the same launch."""
-    items = spec.pack_items["enc"] * (which != "dec") + spec.pack_items["dec"] * (which != "enc")
+    bytes)] buffers cleared by the same launch.  which=None: no packing (the zeroing only)."""
+    items = ([] if which is None else
+             spec.pack_items["enc"] * (which != "dec") + spec.pack_items["dec"] * (which != "enc"))
     if items and zero:
         P.add("cv_pack_conv_weights_zero", struct_array(cv_conv_pack, items), len(items),
               ptr_array([t.data_ptr() for t, _ in zero]), (ctypes.c_size_t * len(zero))(*[nb for _, nb in zero]),

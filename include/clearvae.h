@@ -126,6 +126,15 @@ int cv_pack_conv_weights(const cv_conv_pack* items, int n, cv_stream_t stream);
  * touched by the packing: the first launch of a training step clears the step's accumulators with it. */
 int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void* const* zero_ptrs, const size_t* zero_bytes,
                               int zero_count, cv_stream_t stream);
+/* (cv_pack_conv_weights_zero / _zero_copy accept n = 0 items when they have buffers to zero or copy) */
+/* torch.optim.Adam over a flat parameter arena (cv_adam_step, trainer.py:483) with the weight packing of
+ * cv_pack_conv_weights in the same launch: the packing workgroups update their tile's parameters and pack the new
+ * values (the items' src must lie inside params[0, numel)), the rest of the arena is updated by the launch's other
+ * workgroups; the last workgroup advances step[0] (and aux_counter).  The packed copies are then current for the
+ * next step's forward without a packing launch. */
+int cv_adam_pack_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t numel,
+                      const float* hyper, int64_t* step, const float* grad_scale, int64_t* aux_counter,
+                      const cv_conv_pack* items, int n, cv_stream_t stream);
 /* cv_pack_conv_weights_zero plus up to 4 device copies (16-byte aligned and sized) in the same launch: the fused
  * step's first launch of a replayed step also moves the batch (X, labels: trainer.py:447-450's `X.to(device)` of a
  * device-resident batch) into the step graph's static input buffers, so the copy is not a launch of its own. */
