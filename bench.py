@@ -183,13 +183,22 @@ def isolated_pass(G, reps=20, rounds=3):
     for pname, P in _programs(G):
         for i, (name, fn, args, _lane) in enumerate(P.calls):
             if (fn is None or _lane in ("join", "host")
-                    or name in ("cv_ntxent_aux", "cv_ntxent_aux_combine", "cv_ntxent_aux_flush")):  # (a join; a queue)
+                    or name in ("cv_ntxent_aux_combine", "cv_ntxent_aux_flush")):  # (a join; part of a queued phase)
                 continue
+            # a queued NT-Xent phase is timed on its own: queued (with the combine block attached to it, if the
+            # program attaches one) and launched by a flush, as a step issues it when no launch serves it
+            comb = None
+            if name == "cv_ntxent_aux" and i + 1 < len(P.calls) and P.calls[i + 1][0] == "cv_ntxent_aux_combine":
+                comb = P.calls[i + 1]
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 s = _lib.stream_handle()
                 for _ in range(reps):
                     _lib.check(fn(*args, s), name)
+                    if name == "cv_ntxent_aux":
+                        if comb is not None:
+                            _lib.check(comb[1](*comb[2], s), comb[0])
+                        _lib.check(_lib.lib().cv_ntxent_aux_flush(s), "cv_ntxent_aux_flush")
             g.replay()
             torch.cuda.synchronize()
             best = None
@@ -375,12 +384,24 @@ def call_kernels(G, label):
     P = dict(_programs(G)).get(pname)
     if P is None:
         return None
-    name, fn, cargs, _lane = P.calls[int(rest.split("]")[0])]
+    idx = int(rest.split("]")[0])
+    name, fn, cargs, _lane = P.calls[idx]
+    # the NT-Xent phase queued right before the call (and its attached combine block) is queued again, so a launch
+    # that serves it in the step logs the merged kernel it runs there; a phase it does not serve is dropped unlaunched
+    pre = []
+    j = idx - 1
+    while j >= 0 and P.calls[j][0] in ("cv_ntxent_aux", "cv_ntxent_aux_combine"):
+        pre.insert(0, P.calls[j])
+        j -= 1
     L = _lib.lib()
     torch.cuda.synchronize()
     prev = L.cv_debug_kernel_log(1)
     try:
-        _lib.check(fn(*cargs, _lib.stream_handle()), name)
+        s = _lib.stream_handle()
+        for pn, pf, pa, _pl in pre:
+            _lib.check(pf(*pa, s), pn)
+        _lib.check(fn(*cargs, s), name)
+        L.cv_ntxent_aux_discard()
         torch.cuda.synchronize()
         buf = ctypes.create_string_buffer(1 << 16)
         n = L.cv_debug_kernel_names(buf, len(buf))
