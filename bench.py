@@ -717,6 +717,8 @@ def main():
                     help="profiling mode: after warmup, launch this step-program call (e.g. 'enc[4]') --reps "
                          "times back to back and exit (for rocprofv3 --pmc)")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--list-calls", action="store_true",
+                    help="print every step-program call label with the kernels one launch of it runs (profiling aid)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check without a GPU: the ranks join a gloo group and rank 0 prints the world")
     args = ap.parse_args()
@@ -777,6 +779,17 @@ def main():
             _lib.check(fn(*cargs, s_), name)
         torch.cuda.synchronize()
         print(json.dumps({"only_call": args.only_call, "name": name, "reps": args.reps}))
+        return
+
+    if args.list_calls:  # (each call launched once more, eagerly: mutates the workspace)
+        res = run_workload(args.config, cfg, 0, args.warmup, device, world, rank, detail=False)
+        G = res["eng"].graphs[B]
+        for pname, P in _programs(G):
+            for i, c in enumerate(P.calls):
+                if c[1] is None or c[3] in ("join", "host") or c[0].startswith("cv_ntxent_aux"):
+                    continue
+                label = f"{pname}[{i}]:{c[0]}"
+                print(json.dumps({"label": label, "lane": c[3], "kernels": call_kernels(G, label)}))
         return
 
     res = run_workload(args.config, cfg, args.steps, args.warmup, device, world, rank,
