@@ -199,6 +199,8 @@ def isolated_pass(G, reps=20, rounds=3):
                         if comb is not None:
                             _lib.check(comb[1](*comb[2], s), comb[0])
                         _lib.check(_lib.lib().cv_ntxent_aux_flush(s), "cv_ntxent_aux_flush")
+                if name.endswith("_side"):  # (its weight gradient ran on side stream 1: joined into the capture)
+                    _join_side()
             g.replay()
             torch.cuda.synchronize()
             best = None
@@ -216,6 +218,15 @@ def isolated_pass(G, reps=20, rounds=3):
     return times
 
 
+def _join_side():
+    """The current stream waits for side stream 1 (a call that put work there, *_side)."""
+    from cvhip.plan import _side_stream
+
+    e = torch.cuda.Event()
+    e.record(_side_stream(torch.cuda.current_device(), 1))
+    torch.cuda.current_stream().wait_event(e)
+
+
 def gemm_flops_of(label, G):
     """Algorithmic FLOPs of one conv / linear call from its program position (None for other calls)."""
     pname, rest = label.split("[", 1)
@@ -228,7 +239,8 @@ def gemm_flops_of(label, G):
     # the other weight packing too; cv_convt_output_loss is the last ConvTranspose2d with the loss fused in)
     one = ("cv_conv_forward", "cv_conv_forward_kpack", "cv_convt_output_loss", "cv_conv_backward_data",
            "cv_conv_backward_data_kpack", "cv_conv_backward_weight", "cv_conv_backward_weight_deferred")
-    two = ("cv_conv_backward_deferred", "cv_conv_backward_deferred_kpack")  # backward-data + weight gradient
+    two = ("cv_conv_backward_deferred", "cv_conv_backward_deferred_kpack",  # backward-data + weight gradient
+           "cv_conv_backward_deferred_kpack_side")
     if name in one or name in two:
         g = args[0]._obj
         k = g.kh * g.kw
@@ -264,6 +276,8 @@ def prefix_times(engine, G, labels, reps=20, rounds=3):
             return 0.0
         P = Program()
         P.calls = [c for _, c in flat[:k + 1]]
+        if any(c[0].endswith("_side") for c in P.calls):  # (work left on side stream 1: joined before the end)
+            P.add_join()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             P.run()

@@ -96,7 +96,7 @@ int direct_scatter(const Geo& g, const cv_operand* in, const float* wk, const fl
 // next GEMM-core weight-gradient launch are captured; dual_end issues them as one grid when the pair is served,
 // else back to back (issue = false: drops them, after an error)
 void dual_begin();
-int dual_end(hipStream_t st, bool issue);
+int dual_end(hipStream_t st, bool issue, hipStream_t side = nullptr);
 // the largest weight-gradient tile rows for the current capture (0: no cap)
 int dual_wgrad_bm_cap();
 int direct_gather(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,

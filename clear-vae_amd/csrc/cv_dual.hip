@@ -127,8 +127,10 @@ static int launch_one(const void* kern, dim3 grid, size_t lds, void* arg, hipStr
 
 }  // namespace dual
 
-// Issue the captured launches: one dual grid when the pair is served, else each on its own (direct first).
-static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
+// Issue the captured launches: one dual grid when the pair is served, else each on its own (direct first; the
+// weight gradient on `side` when given: cv_conv_backward_deferred_kpack_side, which has made `side` wait for the
+// work before the call).
+static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st, hipStream_t side = nullptr) {
   using namespace dual;
   if (d.got && g.got && enabled()) {
     const void* fn = lookup(d.key, g.key);
@@ -194,7 +196,7 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st) {
   }
   if (g.got) {
     g.got = false;
-    r = launch_one(g.kern, g.grid, g.lds, &g.a, st, "gemm");
+    r = launch_one(g.kern, g.grid, g.lds, &g.a, side ? side : st, "gemm");
   }
   return r;
 }
@@ -242,14 +244,14 @@ void dual_begin() {
   fast::g_gemm_cap = &t_gcap;
 }
 
-int dual_end(hipStream_t st, bool issue) {
+int dual_end(hipStream_t st, bool issue, hipStream_t side) {
   direct::g_direct_cap = nullptr;
   fast::g_gemm_cap = nullptr;
   if (!issue) {  // (an error between begin and end: nothing captured is launched)
     t_dcap.got = t_gcap.got = false;
     return 0;
   }
-  return dual_issue(t_dcap, t_gcap, st);
+  return dual_issue(t_dcap, t_gcap, st, side);
 }
 
 }  // namespace cv

@@ -1935,6 +1935,54 @@ extern "C" int cv_conv_backward_deferred_kpack(const cv_conv* g, const cv_operan
   return r ? r : r2;
 }
 
+// cv_conv_backward_deferred_kpack with the weight-gradient launch on a second stream (`side`) where the pair is not
+// one dual grid: the layer's weight gradient needs only what the previous layers' launches have written (its input
+// activation and this layer's output gradient), like its backward-data, so it runs beside that and the next
+// layers' backward-data instead of between them.  `side` first waits for the work issued on `stream` before this
+// call (an event; in a capture the side stream joins the graph there), then takes the weight-gradient launch; the
+// caller joins `side` back before anything reads the deferred partials (cv_step_reduce).  A served dual grid, the
+// image-side layer's fused launch and the self-reducing form (whose ticket words are the stream's in-launch split-K
+// workspace) stay on `stream`.
+static hipEvent_t g_side_fork[FIX_MAX_DEV];
+
+extern "C" int cv_conv_backward_deferred_kpack_side(const cv_conv* g, const cv_operand* gout, const float* wpacked,
+                                                    const float* wkpack, float* gin, const cv_epilogue* ep,
+                                                    const cv_operand* in, float* gweight, float* gbias, float* work,
+                                                    size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t side,
+                                                    cv_stream_t stream) {
+  if (g_wgrad_self < 0) {
+    const char* e = getenv("CV_WGRAD_SELF");
+    g_wgrad_self = e ? (atoi(e) != 0) : 0;
+  }
+  if (!side || side == stream || !g || (g->transposed && !gbias) || g_wgrad_self || g_force_generic)
+    return cv_conv_backward_deferred_kpack(g, gout, wpacked, wkpack, gin, ep, in, gweight, gbias, work, work_bytes,
+                                           defer, stream);
+  clear_error();
+  if (check_conv(g) || check_operand(gout, "conv_backward") || check_operand(in, "conv_backward")) return 1;
+  CV_REQUIRE(wpacked && gin && gweight && defer && work, "conv_backward: null weight / gin / gweight / defer / work");
+  int dev = 0;
+  CV_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < FIX_MAX_DEV, "conv_backward_side: no device");
+  if (!g_side_fork[dev] && hipEventCreateWithFlags(&g_side_fork[dev], hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    g_side_fork[dev] = nullptr;
+    set_error("conv_backward_side: event creation failed");
+    return 2;
+  }
+  if (hipEventRecord(g_side_fork[dev], S(stream)) != hipSuccess ||
+      hipStreamWaitEvent(S(side), g_side_fork[dev], 0) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("conv_backward_side: fork of the side stream failed");
+    return 2;
+  }
+  dual_begin();
+  g_wk = wkpack;
+  int r = cv_conv_backward_data(g, gout, wpacked, gin, ep, stream);
+  if (r == 0) r = cv_conv_backward_weight_deferred(g, in, gout, gweight, gbias, work, work_bytes, defer, stream);
+  g_wk = nullptr;
+  const int r2 = dual_end(S(stream), r == 0, S(side));
+  return r ? r : r2;
+}
+
 // ---------------------------------------------------------------- linear layers
 static int linear_launch(Args& a, int accumulate, hipStream_t st) {
   int BM_, BN_;

@@ -187,6 +187,11 @@ _SIGS = {
         [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), _P(cv_operand), c_void_p,
          c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer), c_void_p],
     ),
+    "cv_conv_backward_deferred_kpack_side": (
+        c_int,
+        [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), _P(cv_operand), c_void_p,
+         c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer), c_void_p, c_void_p],
+    ),
     "cv_linear_backward_weight_deferred": (
         c_int,
         [_P(cv_linear), _P(cv_operand), _P(cv_operand), c_void_p, c_void_p, c_void_p, c_size_t, _P(cv_wgrad_defer),

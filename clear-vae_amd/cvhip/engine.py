@@ -138,6 +138,11 @@ MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "2"))
 # node and the copy a launch of its own (A/B)
 PACK_COPY = os.environ.get("CVHIP_PACK_COPY", "1") == "1"
 
+# CVHIP_WGRAD_LANE=1: single-process steps issue the interior layers' deferred weight gradients on side stream 1
+# (Workspace.wgrad_side, cv_conv_backward_deferred_kpack_side): each runs beside its own and the next layers'
+# backward-data launches instead of between them; the `enc` program joins the side stream before cv_step_reduce.
+WGRAD_LANE = int(os.environ.get("CVHIP_WGRAD_LANE", "1"))  # (2: the decoder's first ConvTranspose2d too)
+
 
 def disc_params(disc):
     """The factor discriminator of get_cleartcvae_trainer (trainer_utils.py:133-138) as a parameter list, or
@@ -488,6 +493,8 @@ class ClearStep:
         dp = self.dp
         adam_pack = self.adam_pack
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
+        ws.wgrad_side = WGRAD_LANE >= 1 and not dp
+        ws.wgrad_side_first = WGRAD_LANE >= 2
         dec = Program()
         det_dz = DET_DZ and (side_nt or aux_nt) and not chain_nt and ws.fused_decoder_input()
         ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer,
@@ -575,12 +582,16 @@ class ClearStep:
             upd.add(adam_name, A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                     self.adam.step, self.gscale, self.anneal, *adam_tail)
         elif not FUSED_ADAM:
+            if ws.wgrad_side:
+                enc.add_join()
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
             upd.add(adam_name, A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                     self.adam.step, None, self.anneal, *adam_tail)
         if adam_pack:
             upd.keep.append(pack_arr)
         else:  # single process: the optimizer step rides in the end-of-backward reduction launch
+            if ws.wgrad_side:
+                enc.add_join()
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True,
                                    adam=(A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                                          self.adam.step, self.anneal))

@@ -715,12 +715,22 @@ class Workspace:
     # image-side ConvTranspose2d; CVHIP_FUSED_EDGE_BWD=0: the two calls)
     FUSED_EDGE_BWD = os.environ.get("CVHIP_FUSED_EDGE_BWD", "1") != "0"
 
+    # deferred weight gradients of the interior layers on side stream 1 (cv_conv_backward_deferred_kpack_side), beside
+    # the next layers' backward-data launches; set per workspace by the engine (single-process steps, CVHIP_WGRAD_LANE),
+    # whose programs join side stream 1 before cv_step_reduce
+    wgrad_side = False
+    wgrad_side_first = False  # (also the decoder's first ConvTranspose2d, whose backward-data writes d(h))
+
     def _conv_backward(self, P: "Program", geom, gout, wpacked, wkpack, gin, ep, xin, gw, key, defer):
         if defer is None or not self.FUSED_EDGE_BWD:
             P.add("cv_conv_backward_data_kpack", geom, gout, wpacked, wkpack, gin, ep)
             self._wgrad_call(P, "conv", geom, xin, gout, gw, None, key, defer)
             return
         buf = self._defer_buf("conv", geom, key)
+        if self.wgrad_side and min(geom.c_in, geom.c_out) > 4:
+            P.add("cv_conv_backward_deferred_kpack_side", geom, gout, wpacked, wkpack, gin, ep, xin, gw, None, buf,
+                  buf.numel() * 4, defer.next(), _side_stream(self.device, 1).cuda_stream)
+            return
         P.add("cv_conv_backward_deferred_kpack", geom, gout, wpacked, wkpack, gin, ep, xin, gw, None, buf,
               buf.numel() * 4, defer.next())
 
@@ -941,6 +951,12 @@ class Workspace:
                 ep = ep_bwd(self.bn_dec[li - 1], self.y_dec[li - 1], sp.dec[li - 1].relu)
                 xin = operand(self.y_dec[li - 1], XF_BNRELU, self.bn_dec[li - 1].cv(True))
                 self._conv_backward(P, g, gout, c.wbwd, c.wfwd, self.g_dec[li - 1], ep, xin,
+                                    param_grad(c.mod.weight), ("dec", li), defer)
+                continue
+            elif defer is not None and self.wgrad_side and self.wgrad_side_first and self.FUSED_EDGE_BWD:
+                # (the first ConvTranspose2d's weight gradient on the side stream too: beside the decoder-input
+                # backward and the latent launches that follow)
+                self._conv_backward(P, g, gout, c.wbwd, c.wfwd, self.gah, ep_none(), operand(self.ah),
                                     param_grad(c.mod.weight), ("dec", li), defer)
                 continue
             else:

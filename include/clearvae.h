@@ -204,6 +204,17 @@ int cv_conv_backward_deferred_kpack(const cv_conv* g, const cv_operand* gout, co
                                     const float* wkpack, float* gin, const cv_epilogue* ep, const cv_operand* in,
                                     float* gweight, float* gbias, float* work, size_t work_bytes,
                                     cv_wgrad_defer* defer, cv_stream_t stream);
+/* cv_conv_backward_deferred_kpack with the weight-gradient launch on `side` where the pair is not one dual grid:
+ * `side` waits for the work issued on `stream` before the call (an event; in a capture the side stream joins the
+ * graph there), then runs the weight gradient beside this and the next layers' backward-data launches.  The caller
+ * joins `side` back into `stream` before the deferred partials are read (cv_step_reduce).  Dual grids, the
+ * image-side ConvTranspose2d's fused launch and the self-reducing split (CV_WGRAD_SELF) stay on `stream`;
+ * side = NULL or = stream: cv_conv_backward_deferred_kpack. */
+int cv_conv_backward_deferred_kpack_side(const cv_conv* g, const cv_operand* gout, const float* wpacked,
+                                         const float* wkpack, float* gin, const cv_epilogue* ep,
+                                         const cv_operand* in, float* gweight, float* gbias, float* work,
+                                         size_t work_bytes, cv_wgrad_defer* defer, cv_stream_t side,
+                                         cv_stream_t stream);
 
 /* ---- fully connected layers (nn.Linear heads vae.py:27-30; decoder Linear vae.py:33) ----
  * A linear layer whose input (or output) is the NCHW-flattened view of an NHWC activation with
