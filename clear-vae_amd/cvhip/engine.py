@@ -138,9 +138,12 @@ MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "2"))
 # node and the copy a launch of its own (A/B)
 PACK_COPY = os.environ.get("CVHIP_PACK_COPY", "1") == "1"
 
-# CVHIP_WGRAD_LANE=1: single-process steps issue the interior layers' deferred weight gradients on side stream 1
-# (Workspace.wgrad_side, cv_conv_backward_deferred_kpack_side): each runs beside its own and the next layers'
-# backward-data launches instead of between them; the `enc` program joins the side stream before cv_step_reduce.
+# CVHIP_WGRAD_LANE (default 1): the interior layers' deferred weight gradients on side stream 1 (Workspace.wgrad_side,
+# cv_conv_backward_deferred_kpack_side): each runs beside its own and the next layers' backward-data launches instead
+# of between them; every program joins the side stream before its cv_step_reduce (single process: one, in `enc`;
+# data parallel: one per gradient bucket, so each graph segment ends joined).  Same box, two rounds: CelebA 2.090 ->
+# 2.021 ms, C3 3.814 -> 3.664, C5 bf16 1.208 -> 1.161, PACS 0.870 -> 0.859, MNIST neutral (its pairs are dual
+# grids).  0: one stream.
 WGRAD_LANE = int(os.environ.get("CVHIP_WGRAD_LANE", "1"))  # (2: the decoder's first ConvTranspose2d too)
 
 
@@ -493,7 +496,7 @@ class ClearStep:
         dp = self.dp
         adam_pack = self.adam_pack
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
-        ws.wgrad_side = WGRAD_LANE >= 1 and not dp
+        ws.wgrad_side = WGRAD_LANE >= 1
         ws.wgrad_side_first = WGRAD_LANE >= 2
         dec = Program()
         det_dz = DET_DZ and (side_nt or aux_nt) and not chain_nt and ws.fused_decoder_input()
@@ -502,6 +505,8 @@ class ClearStep:
         if dl_nt:
             dec.keep.append(br_arr)
         if dp:
+            if ws.wgrad_side:
+                dec.add_join()
             ws.step_reduce_program(dec, dec_defer, pg, "dec", running=False)
 
         # latent terms -> d(heads)
@@ -565,10 +570,14 @@ class ClearStep:
             enc_defer2 = DeferGroup()
             ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, layers=range(nl - 1, k - 1, -1),
                                         chain=chain)
+            if ws.wgrad_side:
+                enc.add_join()
             ws.step_reduce_program(enc, enc_defer, pg, ws.bn_enc[k:], running=False)
             enc2 = Program()
             ws.encoder_backward_program(enc2, pg, ws.dheads, x=X, defer=enc_defer2, heads=False,
                                         layers=range(k - 1, -1, -1))
+            if ws.wgrad_side:
+                enc2.add_join()
             ws.step_reduce_program(enc2, enc_defer2, pg, ws.bn_enc[:k], running=False)
             ws.running_program(enc2, "all")
         else:
