@@ -255,11 +255,24 @@ def gemm_flops_of(label, G):
     return None
 
 
+def _one_stream(call):
+    """A step-program call with its side-stream part on the call's own stream: cv_conv_backward_deferred_kpack_side
+    as cv_conv_backward_deferred_kpack (the same kernels, back to back), so a prefix is one stream's chain and the
+    difference of two prefixes is the call's own time, not the side stream's backlog."""
+    name, fn, args, lane = call
+    if name == "cv_conv_backward_deferred_kpack_side":
+        from cvhip import _lib
+
+        return (name[:-5], getattr(_lib.lib(), name[:-5]), list(args[:-1]), lane)
+    return call
+
+
 def prefix_times(engine, G, labels, reps=20, rounds=3):
     """In-graph, in-step duration of the given calls: a graph of the step's calls up to and including call
     i, minus one up to call i-1, each replayed REPS times between HIP events on the launch stream (min of
     ROUNDS).  The step's main-lane calls only (data parallel: the side-lane weight-gradient calls and the
-    collectives between segments are left out, so a prefix is the single-stream chain the call runs in);
+    collectives between segments are left out, so a prefix is the single-stream chain the call runs in; a call
+    that puts its weight gradient on side stream 1 runs both launches on the stream here, _one_stream);
     labels on a side lane are not timed.  Mutates the workspace (run after timing)."""
     from cvhip.plan import Program
 
@@ -275,9 +288,7 @@ def prefix_times(engine, G, labels, reps=20, rounds=3):
         if k < 0:
             return 0.0
         P = Program()
-        P.calls = [c for _, c in flat[:k + 1]]
-        if any(c[0].endswith("_side") for c in P.calls):  # (work left on side stream 1: joined before the end)
-            P.add_join()
+        P.calls = [_one_stream(c) for _, c in flat[:k + 1]]
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             P.run()
