@@ -1977,7 +1977,10 @@ extern "C" int cv_conv_backward_deferred_kpack_side(const cv_conv* g, const cv_o
   dual_begin();
   g_wk = wkpack;
   int r = cv_conv_backward_data(g, gout, wpacked, gin, ep, stream);
-  if (r == 0) r = cv_conv_backward_weight_deferred(g, in, gout, gweight, gbias, work, work_bytes, defer, stream);
+  // (the weight gradient's own stream is `side`: a launch path the dual capture does not take — the generic core,
+  // the edge kernels — issues there directly; a captured one is issued by dual_end, on `stream` inside a served dual
+  // grid, else on `side`)
+  if (r == 0) r = cv_conv_backward_weight_deferred(g, in, gout, gweight, gbias, work, work_bytes, defer, side);
   g_wk = nullptr;
   const int r2 = dual_end(S(stream), r == 0, S(side));
   return r ? r : r2;
