@@ -1954,7 +1954,8 @@ extern "C" int cv_conv_backward_deferred_kpack_side(const cv_conv* g, const cv_o
     const char* e = getenv("CV_WGRAD_SELF");
     g_wgrad_self = e ? (atoi(e) != 0) : 0;
   }
-  if (!side || side == stream || !g || (g->transposed && !gbias) || g_wgrad_self || g_force_generic)
+  // (the image-side layers — <= 4 channels on one side — take the edge kernels' fused launch: on `stream`)
+  if (!side || side == stream || !g || (g->c_in <= 4 || g->c_out <= 4) || g_wgrad_self || g_force_generic)
     return cv_conv_backward_deferred_kpack(g, gout, wpacked, wkpack, gin, ep, in, gweight, gbias, work, work_bytes,
                                            defer, stream);
   clear_error();
