@@ -199,8 +199,8 @@ def isolated_pass(G, reps=20, rounds=3):
                         if comb is not None:
                             _lib.check(comb[1](*comb[2], s), comb[0])
                         _lib.check(_lib.lib().cv_ntxent_aux_flush(s), "cv_ntxent_aux_flush")
-                if name.endswith("_side"):  # (its weight gradient ran on side stream 1: joined into the capture)
-                    _join_side()
+                if name.endswith("_side"):  # (its weight gradient ran on a side stream: joined into the capture)
+                    _join_side(args[-1])
             g.replay()
             torch.cuda.synchronize()
             best = None
@@ -218,12 +218,10 @@ def isolated_pass(G, reps=20, rounds=3):
     return times
 
 
-def _join_side():
-    """The current stream waits for side stream 1 (a call that put work there, *_side)."""
-    from cvhip.plan import _side_stream
-
+def _join_side(handle):
+    """The current stream waits for the side stream `handle` (a call that put work there, *_side)."""
     e = torch.cuda.Event()
-    e.record(_side_stream(torch.cuda.current_device(), 1))
+    e.record(torch.cuda.ExternalStream(handle))
     torch.cuda.current_stream().wait_event(e)
 
 

@@ -138,13 +138,17 @@ MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "2"))
 # node and the copy a launch of its own (A/B)
 PACK_COPY = os.environ.get("CVHIP_PACK_COPY", "1") == "1"
 
-# CVHIP_WGRAD_LANE (default 1): the interior layers' deferred weight gradients on side stream 1 (Workspace.wgrad_side,
-# cv_conv_backward_deferred_kpack_side): each runs beside its own and the next layers' backward-data launches instead
-# of between them; every program joins the side stream before its cv_step_reduce (single process: one, in `enc`;
-# data parallel: one per gradient bucket, so each graph segment ends joined).  Same box, two rounds: CelebA 2.090 ->
-# 2.021 ms, C3 3.814 -> 3.664, C5 bf16 1.208 -> 1.161, PACS 0.870 -> 0.859, MNIST neutral (its pairs are dual
-# grids).  0: one stream.
-WGRAD_LANE = int(os.environ.get("CVHIP_WGRAD_LANE", "1"))  # (2: the decoder's first ConvTranspose2d too)
+# CVHIP_WGRAD_LANE (default 2): the deferred weight gradients of the conv / convT layers off the image (the image-side
+# layers keep their fused edge launches) on side stream 1 (Workspace.wgrad_side, cv_conv_backward_deferred_kpack_side):
+# each runs beside its own and the next layers' backward-data launches instead of between them; every program joins
+# the side stream before its cv_step_reduce (single process: once, in `enc`; data parallel: once per gradient bucket,
+# so each graph segment ends joined).  Same box, two rounds: CelebA 2.089 -> 1.930 ms, C3 3.811 -> 3.582, C5 bf16
+# 1.209 -> 1.110, its fp32 twin 1.423 -> 1.330, PACS 0.869 -> 0.808, MNIST neutral (its pairs are dual grids, which
+# stay on the step's stream); 2 adds the decoder's first ConvTranspose2d (beside the latent launches): CelebA 1.928
+# -> 1.887, C3 3.581 -> 3.532, C5 1.112 -> 1.097, PACS 0.805 -> 0.800.  1: without it; 0: one stream.
+# CVHIP_WGRAD_LANES=2 (two side streams in rotation) measured neutral to slower (C5 1.112 -> 1.170 ms): default 1.
+WGRAD_LANE = int(os.environ.get("CVHIP_WGRAD_LANE", "2"))  # (2: the decoder's first ConvTranspose2d too; 1: not it)
+WGRAD_LANES = max(1, int(os.environ.get("CVHIP_WGRAD_LANES", "1")))  # side streams the weight gradients rotate over
 
 
 def disc_params(disc):
@@ -498,6 +502,8 @@ class ClearStep:
         dec_defer, enc_defer = DeferGroup(), DeferGroup()
         ws.wgrad_side = WGRAD_LANE >= 1
         ws.wgrad_side_first = WGRAD_LANE >= 2
+        ws.wgrad_lanes = WGRAD_LANES
+        ws._wside_next = 0
         dec = Program()
         det_dz = DET_DZ and (side_nt or aux_nt) and not chain_nt and ws.fused_decoder_input()
         ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer if dp else enc_defer,
@@ -506,7 +512,7 @@ class ClearStep:
             dec.keep.append(br_arr)
         if dp:
             if ws.wgrad_side:
-                dec.add_join()
+                dec.add_join(ws.side_lanes())
             ws.step_reduce_program(dec, dec_defer, pg, "dec", running=False)
 
         # latent terms -> d(heads)
@@ -571,13 +577,13 @@ class ClearStep:
             ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer, layers=range(nl - 1, k - 1, -1),
                                         chain=chain)
             if ws.wgrad_side:
-                enc.add_join()
+                enc.add_join(ws.side_lanes())
             ws.step_reduce_program(enc, enc_defer, pg, ws.bn_enc[k:], running=False)
             enc2 = Program()
             ws.encoder_backward_program(enc2, pg, ws.dheads, x=X, defer=enc_defer2, heads=False,
                                         layers=range(k - 1, -1, -1))
             if ws.wgrad_side:
-                enc2.add_join()
+                enc2.add_join(ws.side_lanes())
             ws.step_reduce_program(enc2, enc_defer2, pg, ws.bn_enc[:k], running=False)
             ws.running_program(enc2, "all")
         else:
@@ -592,7 +598,7 @@ class ClearStep:
                     self.adam.step, self.gscale, self.anneal, *adam_tail)
         elif not FUSED_ADAM:
             if ws.wgrad_side:
-                enc.add_join()
+                enc.add_join(ws.side_lanes())
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
             upd.add(adam_name, A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                     self.adam.step, None, self.anneal, *adam_tail)
@@ -600,7 +606,7 @@ class ClearStep:
             upd.keep.append(pack_arr)
         else:  # single process: the optimizer step rides in the end-of-backward reduction launch
             if ws.wgrad_side:
-                enc.add_join()
+                enc.add_join(ws.side_lanes())
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True,
                                    adam=(A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                                          self.adam.step, self.anneal))

@@ -468,9 +468,10 @@ class Program:
         it; a later add_join, in this or a later program, joins it back)."""
         self.calls.append((name, getattr(_lib.lib(), name), self._conv(args), 1))
 
-    def add_join(self):
-        """The main stream waits here for everything issued on the side lanes so far."""
-        self.calls.append((JOIN, None, [], JOIN))
+    def add_join(self, lanes=()):
+        """The main stream waits here for everything issued on the side lanes so far (and on `lanes`: side lanes a
+        C-ABI call of this or an earlier program put work on, e.g. cv_conv_backward_deferred_kpack_side)."""
+        self.calls.append((JOIN, None, list(lanes), JOIN))
 
     def add_host(self, name: str, fn, *args):
         """fn(*args) on the host when the program is enqueued (eagerly, or while a graph is captured)."""
@@ -522,11 +523,11 @@ class Program:
         forked = {}  # side lane -> forked since the main stream's last call (no new fork needed)
         active = []  # side lanes forked in this run, not yet joined
 
-        def join_all():
+        def join_all(extra=()):
             nonlocal ev
             # (a join with no side lane forked in this run joins side lane 1: a fork left open by an earlier
             # program, join_at_end=False)
-            for k in (active or [1]):
+            for k in (sorted(set(active) | set(extra)) or [1]):
                 e = self._event(ev)
                 ev += 1
                 e.record(_side_stream(main.device, k))
@@ -536,7 +537,7 @@ class Program:
 
         for i, (name, fn, args, lane) in enumerate(self.calls):
             if lane == JOIN:
-                join_all()
+                join_all(args)
                 continue
             if lane == HOST:
                 fn(*args)
@@ -720,6 +721,12 @@ class Workspace:
     # whose programs join side stream 1 before cv_step_reduce
     wgrad_side = False
     wgrad_side_first = False  # (also the decoder's first ConvTranspose2d, whose backward-data writes d(h))
+    wgrad_lanes = 1  # side streams the weight gradients rotate over (1, 2, ...)
+    _wside_next = 0
+
+    def side_lanes(self):
+        """The side lanes the weight gradients of this workspace's programs use (joined before cv_step_reduce)."""
+        return list(range(1, self.wgrad_lanes + 1)) if self.wgrad_side else []
 
     def _conv_backward(self, P: "Program", geom, gout, wpacked, wkpack, gin, ep, xin, gw, key, defer):
         if defer is None or not self.FUSED_EDGE_BWD:
@@ -728,8 +735,10 @@ class Workspace:
             return
         buf = self._defer_buf("conv", geom, key)
         if self.wgrad_side and min(geom.c_in, geom.c_out) > 4:
+            lane = 1 + self._wside_next % self.wgrad_lanes
+            self._wside_next += 1
             P.add("cv_conv_backward_deferred_kpack_side", geom, gout, wpacked, wkpack, gin, ep, xin, gw, None, buf,
-                  buf.numel() * 4, defer.next(), _side_stream(self.device, 1).cuda_stream)
+                  buf.numel() * 4, defer.next(), _side_stream(self.device, lane).cuda_stream)
             return
         P.add("cv_conv_backward_deferred_kpack", geom, gout, wpacked, wkpack, gin, ep, xin, gw, None, buf,
               buf.numel() * 4, defer.next())
