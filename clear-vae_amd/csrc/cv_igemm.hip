@@ -679,6 +679,7 @@ struct PackArgs {
   long plain0[2 * MAX_PACK + 2];
   long plainn[2 * MAX_PACK + 2];
   int nplain;
+  int hold;  // 1: the last workgroup leaves step[0] / aux as they are (a first part of a split update)
 };
 
 // Adam constants of the step (the arithmetic of adam_kernel, cv_mi.hip); computed by thread 0 into sh[8]
@@ -716,9 +717,11 @@ __device__ __forceinline__ void adam_arrive(const PackArgs& a, int* flag) {
   }
   __syncthreads();
   if (*flag && threadIdx.x == 0) {
-    a.step[0] += 1;
+    if (!a.hold) {
+      a.step[0] += 1;
+      if (a.aux) a.aux[0] += 1;
+    }
     a.step[1] = 0;
-    if (a.aux) a.aux[0] += 1;
   }
 }
 // the slice workgroups of an Adam launch: the arena ranges no packed item covers
@@ -1678,6 +1681,7 @@ static int pack_launch(const cv_conv_pack* items, int n, void* const* zptrs, con
     a.ad = 1;
     a.ap = adam->ap; a.ag = adam->ag; a.am = adam->am; a.av = adam->av;
     a.hyper = adam->hyper; a.step = adam->step; a.gscale = adam->gscale; a.aux = adam->aux;
+    a.hold = adam->hold;
     a.nplain = adam->nplain;
     for (int i = 0; i < adam->nplain; ++i) { a.plain0[i] = adam->plain0[i]; a.plainn[i] = adam->plainn[i]; }
   }
@@ -1759,9 +1763,28 @@ extern "C" int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void*
   return pack_launch(items, n, zero_ptrs, zero_bytes, zero_count, stream);
 }
 
+static int adam_pack_part(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t numel,
+                          const float* hyper, int64_t* step, const float* grad_scale, int64_t* aux_counter,
+                          const cv_conv_pack* items, int n, int advance, cv_stream_t stream);
+
 extern "C" int cv_adam_pack_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                                  int64_t numel, const float* hyper, int64_t* step, const float* grad_scale,
                                  int64_t* aux_counter, const cv_conv_pack* items, int n, cv_stream_t stream) {
+  return adam_pack_part(params, grads, exp_avg, exp_avg_sq, numel, hyper, step, grad_scale, aux_counter, items, n, 1,
+                        stream);
+}
+
+extern "C" int cv_adam_pack_step_part(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                                      int64_t numel, const float* hyper, int64_t* step, const float* grad_scale,
+                                      int64_t* aux_counter, const cv_conv_pack* items, int n, int advance,
+                                      cv_stream_t stream) {
+  return adam_pack_part(params, grads, exp_avg, exp_avg_sq, numel, hyper, step, grad_scale, aux_counter, items, n,
+                        advance, stream);
+}
+
+static int adam_pack_part(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t numel,
+                          const float* hyper, int64_t* step, const float* grad_scale, int64_t* aux_counter,
+                          const cv_conv_pack* items, int n, int advance, cv_stream_t stream) {
   clear_error();
   CV_REQUIRE(params && grads && exp_avg && exp_avg_sq && hyper && step && numel > 0 && items && n > 0 &&
                  n <= MAX_PACK, "adam_pack_step: bad args");
@@ -1783,6 +1806,7 @@ extern "C" int cv_adam_pack_step(float* params, const float* grads, float* exp_a
   memset(&ad, 0, sizeof(ad));
   ad.ap = params; ad.ag = grads; ad.am = exp_avg; ad.av = exp_avg_sq;
   ad.hyper = hyper; ad.step = step; ad.gscale = grad_scale; ad.aux = aux_counter;
+  ad.hold = advance ? 0 : 1;
   long cur = 0;
   for (int k = 0; k < n; ++k) {
     const int i = ord[k];

@@ -160,6 +160,9 @@ _SIGS = {
     "cv_adam_pack_step": (
         c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                 _P(cv_conv_pack), c_int, c_void_p]),
+    "cv_adam_pack_step_part": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                _P(cv_conv_pack), c_int, c_int, c_void_p]),
     "cv_pack_conv_weights_zero_copy": (
         c_int, [_P(cv_conv_pack), c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "cv_conv_forward": (c_int, [_P(cv_conv), _P(cv_operand), c_void_p, c_void_p, c_void_p, _P(cv_epilogue), c_void_p]),

@@ -111,14 +111,19 @@ LATENT_CHAIN = os.environ.get("CVHIP_LATENT_CHAIN", "0") == "1"
 # grids 6 + 4 us (0.4735 -> 0.4820 ms with them there: CVHIP_LATENT_AUX_DL=2 forces it).
 LATENT_AUX_DL = int(os.environ.get("CVHIP_LATENT_AUX_DL", "1"))
 
-# CVHIP_ADAM_PACK (default 1; single GPU and data parallel, not with CVHIP_FUSED_ADAM): the VAE's Adam step packs the
+# CVHIP_ADAM_PACK (default auto: on for arenas of >= 2^20 parameters, i.e. VAE64; 1 / 0 force; single GPU and data
+# parallel, not with CVHIP_FUSED_ADAM): the VAE's Adam step packs the
 # conv weights it has just updated in the same launch (cv_adam_pack_step), so the packed copies are current when the
 # next forward starts: a replayed step's first launch only zeroes (and copies the batch), and CLEAR-MIM's / CLEAR-TC's
 # estimator forwards after the update need no packing launch.  Parameters changed outside the engine between steps
 # (load_state_dict, torch optimizers, writes into the arena buffer: anything that bumps a parameter's or the arena's
 # version counter) are repacked before the next replay; changes through a parameter's `.data` alias bypass the
 # counters: call ClearStep.invalidate_packed() after them.
-ADAM_PACK = os.environ.get("CVHIP_ADAM_PACK", "1") == "1"
+# Measured (same box, two rounds, after fixing the CVHIP_ADAM_PACK=0 programs, which had run the reduction and the
+# optimizer twice): MNIST 0.4724 ms unfused vs 0.4842 fused, CelebA 1.8986 vs 1.8888 — the packing launch at the step
+# start costs the small model less than the packing workgroups inside its Adam launch.
+ADAM_PACK = os.environ.get("CVHIP_ADAM_PACK", "auto")
+ADAM_PACK_MIN = 1 << 20
 
 # CVHIP_DET_DZ (default 1; the LATENT_AUX / LATENT_SIDE schedules): the decoder-input gradient dz = d(h) W is computed
 # by the latent combine launch (cv_latent_combine_dz, fixed-order sums) instead of as fp32-atomic partials in the
@@ -149,6 +154,12 @@ PACK_COPY = os.environ.get("CVHIP_PACK_COPY", "1") == "1"
 # CVHIP_WGRAD_LANES=2 (two side streams in rotation) measured neutral to slower (C5 1.112 -> 1.170 ms): default 1.
 WGRAD_LANE = int(os.environ.get("CVHIP_WGRAD_LANE", "2"))  # (2: the decoder's first ConvTranspose2d too; 1: not it)
 WGRAD_LANES = max(1, int(os.environ.get("CVHIP_WGRAD_LANES", "1")))  # side streams the weight gradients rotate over
+
+# CVHIP_SPLIT_UPDATE=1: single-process steps with side-stream weight gradients reduce and update the decoder's
+# parameters (cv_step_reduce of the decoder bucket, cv_adam_pack_step_part over the arena's decoder tail) on side
+# lane 2 as soon as the step has read them (after the latent launches), beside the encoder backward; the encoder's
+# reduction and Adam part (which advances the step counters) stay at the end.
+SPLIT_UPDATE = os.environ.get("CVHIP_SPLIT_UPDATE", "0") == "1"
 
 
 def disc_params(disc):
@@ -302,7 +313,9 @@ class ClearStep:
         self.capture_collectives = GRAPH_COLLECTIVES and self.dp
         # the VAE's Adam launch also packs the conv weights (ADAM_PACK); _packed_sig: the parameters' version
         # counters when the packed copies were last made current (None: unknown, pack before the next replay)
-        self.adam_pack = ADAM_PACK and not (FUSED_ADAM and not self.dp)
+        ap = ADAM_PACK
+        ap = (ap in (True, "1") or (ap not in (False, "0") and self.arena.numel >= ADAM_PACK_MIN))
+        self.adam_pack = ap and not (FUSED_ADAM and not self.dp)
         self._packed_sig = None
         if self.world > 1:  # a noise stream per rank (the shards are different samples; equal noise would tie them)
             self.seed = (self.seed ^ (0x9E3779B97F4A7C15 * cvdist.rank())) & 0xFFFFFFFFFFFFFFFF
@@ -602,14 +615,48 @@ class ClearStep:
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True)
             upd.add(adam_name, A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                     self.adam.step, None, self.anneal, *adam_tail)
-        if adam_pack:
-            upd.keep.append(pack_arr)
         else:  # single process: the optimizer step rides in the end-of-backward reduction launch
             if ws.wgrad_side:
                 enc.add_join(ws.side_lanes())
             ws.step_reduce_program(enc, enc_defer, pg, "all", running=True,
                                    adam=(A.flat, A.grad, self.adam.m, self.adam.v, A.numel, self.adam.hyper,
                                          self.adam.step, self.anneal))
+        if adam_pack:
+            upd.keep.append(pack_arr)
+        # the split update (SPLIT_UPDATE): the decoder bucket's reduction and Adam on side lane 2 once the step has
+        # read the decoder's parameters (after `lat`), beside the encoder backward; `dec_p` / `enc_p` / `upd_p` keep
+        # the one-update form for steps with a before_update hook (which reads the pre-update decoder BatchNorm)
+        dec_p, enc_p, upd_p = dec, enc, upd
+        split = self._split_update_plan(ws, sp, A) if (SPLIT_UPDATE and adam_pack and ws.wgrad_side and not dp
+                                                       and not FUSED_ADAM) else None
+        if split is not None:
+            dec_off, dec_items, enc_items = split
+            dec_defer_s, enc_defer_s = DeferGroup(), DeferGroup()
+            ws._wside_next = 0
+            dec = Program()
+            ws.decoder_backward_program(dec, pg, ws.dz, zero_dz=False, defer=dec_defer_s,
+                                        aux_in=aux_args[1] if dl_nt else None, dz_later=det_dz)
+            if dl_nt:
+                dec.keep.append(br_arr)
+            enc = Program()
+            enc.add_join([1])  # (the decoder's weight gradients, issued on side lane 1 by the `dec` calls)
+            side = Program()
+            ws.step_reduce_program(side, dec_defer_s, pg, "dec", running=True)
+            darr = struct_array(cv_conv_pack, dec_items)
+            f4 = 4 * dec_off
+            side.add("cv_adam_pack_step_part", A.flat.data_ptr() + f4, A.grad.data_ptr() + f4,
+                     self.adam.m.data_ptr() + f4, self.adam.v.data_ptr() + f4, A.numel - dec_off, self.adam.hyper,
+                     self.adam.step, None, self.anneal, darr, len(dec_items), 0)
+            side.keep.append(darr)
+            enc.extend(side, lane=2)
+            ws.encoder_backward_program(enc, pg, ws.dheads, x=X, defer=enc_defer_s, chain=chain)
+            enc.add_join(ws.side_lanes() + [2])
+            ws.step_reduce_program(enc, enc_defer_s, pg, ws.bn_enc, running=True)
+            upd = Program()
+            earr = struct_array(cv_conv_pack, enc_items)
+            upd.add("cv_adam_pack_step_part", A.flat, A.grad, self.adam.m, self.adam.v, dec_off, self.adam.hyper,
+                    self.adam.step, None, self.anneal, earr, len(enc_items), 1)
+            upd.keep.append(earr)
         learn = learn_inj = None
         if self.mode == "mim":
             E = self.est_arena
@@ -755,8 +802,29 @@ class ClearStep:
 
             learn, learn_inj = make_tc(False), make_tc(True)
         return dict(ws=ws, X=X, lab=lab, fwd=fwd, dec=dec, lat=lat, enc=enc, enc2=enc2, upd=upd, learn=learn,
+                    dec_p=dec_p, enc_p=enc_p, upd_p=upd_p,
                     fwd_inj=fwd_inj, lat_inj=lat_inj, learn_inj=learn_inj, eps_buf=eps_buf, perm_buf=perm_buf,
                     fwd_g=fwd_g, pack_call=pack_call)
+
+    def _split_update_plan(self, ws, sp, A):
+        """(decoder arena offset, decoder pack items, encoder pack items) when the decoder's parameters are the
+        arena's tail and every pack item lies on its side of that offset (the split update's two Adam parts), else
+        None."""
+        base = A.flat.data_ptr()
+        dec_params = [p for k, p in self.vae.named_parameters() if k.startswith("decoder.")]
+        if not dec_params:
+            return None
+        dec_ids = {id(p) for p in dec_params}
+        dec_off = min((p.data_ptr() - base) // 4 for p in dec_params)
+        for p in A.params:
+            if (((p.data_ptr() - base) // 4) >= dec_off) != (id(p) in dec_ids):
+                return None
+        ei, di = sp.pack_items["enc"], sp.pack_items["dec"]
+        if not ei or not di:
+            return None
+        if any(it.src - base < 4 * dec_off for it in di) or any(it.src - base >= 4 * dec_off for it in ei):
+            return None
+        return dec_off, di, ei
 
     def _disc_struct(self) -> cv_tc_disc:
         l0w, l0b, l2w, l2b = self.est_arena.params
@@ -845,6 +913,11 @@ class ClearStep:
         self.comm_probe.append(("vae" if buckets is self.buckets else "est", e0, e1))
 
     def _run_eager(self, G, inject=False, before_update=None):
+        if before_update is not None and G.get("dec_p") is not None and G["dec_p"] is not G["dec"]:
+            # (the one-update programs: the hook reads the step's state before any parameter moves)
+            H = dict(G, dec=G["dec_p"], enc=G["enc_p"], upd=G["upd_p"])
+            self._run_segments(self._segments(H, inject), upd=H["upd"], before_update=before_update)
+            return
         self._run_segments(self._segments(G, inject), upd=G["upd"], before_update=before_update)
 
     def _take_injections(self, G) -> bool:

@@ -135,6 +135,14 @@ int cv_pack_conv_weights_zero(const cv_conv_pack* items, int n, void* const* zer
 int cv_adam_pack_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t numel,
                       const float* hyper, int64_t* step, const float* grad_scale, int64_t* aux_counter,
                       const cv_conv_pack* items, int n, cv_stream_t stream);
+/* cv_adam_pack_step over a part of the arena (params .. params + numel, the items inside it) that leaves the step
+ * counters as they are when advance = 0: a split update whose parts run at different points of the step (the
+ * decoder's parameters as soon as the step has read them, beside the encoder backward); the part with advance = 1
+ * (issued after the others, same step) advances step[0] and aux_counter.  Every part computes the bias correction
+ * from the same step[0]. */
+int cv_adam_pack_step_part(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t numel,
+                           const float* hyper, int64_t* step, const float* grad_scale, int64_t* aux_counter,
+                           const cv_conv_pack* items, int n, int advance, cv_stream_t stream);
 /* cv_pack_conv_weights_zero plus up to 4 device copies (16-byte aligned and sized) in the same launch: the fused
  * step's first launch of a replayed step also moves the batch (X, labels: trainer.py:447-450's `X.to(device)` of a
  * device-resident batch) into the step graph's static input buffers, so the copy is not a launch of its own. */
