@@ -97,6 +97,9 @@ int direct_scatter(const Geo& g, const cv_operand* in, const float* wk, const fl
 // else back to back (issue = false: drops them, after an error)
 void dual_begin();
 int dual_end(hipStream_t st, bool issue, hipStream_t side = nullptr);
+// the capture between dual_begin and dual_end will issue its weight gradient on a side stream (tile plan without the
+// dual grid's row cap where no dual grid will be served)
+void dual_side(bool on);
 // the largest weight-gradient tile rows for the current capture (0: no cap)
 int dual_wgrad_bm_cap();
 int direct_gather(const Geo& g, const cv_operand* in, const float* wk, const float* bias, float* out,

@@ -130,9 +130,23 @@ static int launch_one(const void* kern, dim3 grid, size_t lds, void* arg, hipStr
 // Issue the captured launches: one dual grid when the pair is served, else each on its own (direct first; the
 // weight gradient on `side` when given: cv_conv_backward_deferred_kpack_side, which has made `side` wait for the
 // work before the call).
+// With a side stream the weight gradient overlaps this and the next layers' backward-data as its own launch, which
+// beats the dual grid on the larger pairs (same box, two rounds: MNIST 0.4735 -> 0.4439 ms, CelebA 1.893 -> 1.845,
+// C3 3.542 -> 3.497; PACS 0.804 -> 0.809 and C5 bf16 1.095 -> 1.100 slightly slower): a dual grid is then served only
+// below side_dual_max() direct workgroups (CV_SIDE_DUAL_MAX, default 256; 0: never).
+static long side_dual_max() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_SIDE_DUAL_MAX");
+    v = e ? atol(e) : 256;
+    if (v < 0) v = 0;
+  }
+  return v;
+}
+
 static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st, hipStream_t side = nullptr) {
   using namespace dual;
-  if (d.got && g.got && enabled()) {
+  if (d.got && g.got && enabled() && (!side || (long)d.grid.x * d.grid.y < side_dual_max())) {
     const void* fn = lookup(d.key, g.key);
     const long nd = (long)d.grid.x * d.grid.y, ng = (long)g.grid.x * g.grid.y * g.grid.z;
     // (a direct grid of more than one resident round — VAE64's conv2 at 256 images, 1024 workgroups — measured
@@ -204,9 +218,14 @@ static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st, hi
 static thread_local direct::DirectCap t_dcap;
 static thread_local fast::GemmCap t_gcap;
 
+static thread_local bool t_side = false;  // (this capture issues the weight gradient on a side stream)
+void dual_side(bool on) { t_side = on; }
+
 int dual_wgrad_bm_cap() {  // (only when the captured direct launch belongs to a served pair)
   if (!direct::g_direct_cap || !t_dcap.got || !dual::enabled()) return 0;
-  return ((long)t_dcap.grid.x * t_dcap.grid.y <= dual::max_direct() && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
+  const long nd = (long)t_dcap.grid.x * t_dcap.grid.y;
+  if (t_side && nd >= side_dual_max()) return 0;
+  return (nd <= dual::max_direct() && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
 }
 
 // Workgroup slots the weight-gradient role of a served dual grid has in the grid's first resident round (0: no

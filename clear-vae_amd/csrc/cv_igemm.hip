@@ -2000,6 +2000,7 @@ extern "C" int cv_conv_backward_deferred_kpack_side(const cv_conv* g, const cv_o
     return 2;
   }
   dual_begin();
+  dual_side(true);
   g_wk = wkpack;
   int r = cv_conv_backward_data(g, gout, wpacked, gin, ep, stream);
   // (the weight gradient's own stream is `side`: a launch path the dual capture does not take — the generic core,
@@ -2007,6 +2008,7 @@ extern "C" int cv_conv_backward_deferred_kpack_side(const cv_conv* g, const cv_o
   // grid, else on `side`)
   if (r == 0) r = cv_conv_backward_weight_deferred(g, in, gout, gweight, gbias, work, work_bytes, defer, side);
   g_wk = nullptr;
+  dual_side(false);
   const int r2 = dual_end(S(stream), r == 0, S(side));
   return r ? r : r2;
 }
