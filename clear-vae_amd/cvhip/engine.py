@@ -131,14 +131,14 @@ ADAM_PACK_MIN = 1 << 20
 # bit-identical (tests/test_gpu_determinism.py); 0: the atomic partials (A/B)
 DET_DZ = os.environ.get("CVHIP_DET_DZ", "1") == "1"
 
-# CVHIP_MIM_BRANCHES (default 3; 0: the sequential form): CLEAR-MIM's five estimator-update decoder forwards
+# CVHIP_MIM_BRANCHES (default 2; 0: the sequential form): CLEAR-MIM's five estimator-update decoder forwards
 # (trainer.py:873-888) on this many side lanes of the single-GPU step graph, beside the five estimator learning steps
 # on the step's stream (ClearStep._programs, make_learn_branched).  Measured (round 6, VAE64 n = 256, the five
 # decoder forwards alone in a graph, scratch experiment): back to back 1.50 ms; on 5 / 3 / 2 lanes 1.23 / 1.20 /
 # 1.25 ms; one decoder pass over 5 x 256 images (the bound of a segmented-statistics kernel) 1.27 ms.  In the step,
-# with the side-stream weight gradients of the VAE step (WGRAD_LANE): 1 / 2 / 3 lanes 3.730 / 3.511 / 3.480 ms (same
-# box, two rounds; before them 2 lanes won, 3.92 vs 3.95-3.99 ms).
-MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "3"))
+# with the side-stream weight gradients of the VAE step (WGRAD_LANE): 1 / 2 / 3 lanes 3.730 / 3.511 / 3.480 ms on one
+# box (two rounds), 2 / 3 lanes 3.497 / 3.529 ms on another: 2 and 3 within the boxes' spread, 2 kept.
+MIM_BRANCHES = int(os.environ.get("CVHIP_MIM_BRANCHES", "2"))
 
 # CVHIP_PACK_COPY (default 1): a replayed step's first launch (weight packing + step zeroing) is issued eagerly before
 # the step graph with the batch copy folded in (cv_pack_conv_weights_zero_copy); 0: the packing is the graph's first
