@@ -143,10 +143,24 @@ static long side_dual_max() {
   }
   return v;
 }
+// ... or at batches of at most side_dual_n() images (CV_SIDE_DUAL_N, default 32: PACS's shard, 0.8015 -> 0.7955 ms
+// with its conv2 pair dual; at 128 the C5 fp32 twin lost 3 % that way, 1.268 -> 1.307 ms, and bf16 was neutral)
+static int side_dual_n() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CV_SIDE_DUAL_N");
+    v = e ? atoi(e) : 32;
+    if (v < 0) v = 0;
+  }
+  return v;
+}
+static bool side_keeps_dual(const direct::DirectCap& d) {
+  return (long)d.grid.x * d.grid.y < side_dual_max() || d.a.g.n <= side_dual_n();
+}
 
 static int dual_issue(direct::DirectCap& d, fast::GemmCap& g, hipStream_t st, hipStream_t side = nullptr) {
   using namespace dual;
-  if (d.got && g.got && enabled() && (!side || (long)d.grid.x * d.grid.y < side_dual_max())) {
+  if (d.got && g.got && enabled() && (!side || side_keeps_dual(d))) {
     const void* fn = lookup(d.key, g.key);
     const long nd = (long)d.grid.x * d.grid.y, ng = (long)g.grid.x * g.grid.y * g.grid.z;
     // (a direct grid of more than one resident round — VAE64's conv2 at 256 images, 1024 workgroups — measured
@@ -224,7 +238,7 @@ void dual_side(bool on) { t_side = on; }
 int dual_wgrad_bm_cap() {  // (only when the captured direct launch belongs to a served pair)
   if (!direct::g_direct_cap || !t_dcap.got || !dual::enabled()) return 0;
   const long nd = (long)t_dcap.grid.x * t_dcap.grid.y;
-  if (t_side && nd >= side_dual_max()) return 0;
+  if (t_side && !side_keeps_dual(t_dcap)) return 0;
   return (nd <= dual::max_direct() && dual::lookup(t_dcap.key, nullptr)) ? 64 : 0;
 }
 
