@@ -1544,7 +1544,16 @@ static int run_wgrad(const Geo& g, const cv_operand* small, const cv_operand* bi
   a.N = g.kh * g.kw * g.cb;
   CV_REQUIRE(!gbias || (a.N % 4) == 0, "wgrad: bias column needs taps*channels % 4 == 0");
   a.K = g.n * g.hs * g.ws;
-  WPlan w = wgrad_plan(a.M, a.N, a.K, split_k);
+  // bf16 contractions aim their K split at fewer workgroups (CV_WGRAD_TARGET_BF16, default 512; the fp32 default
+  // stays 1024): with the weight gradients beside the backward-data on a side stream, C5's bf16 shard 1.090 -> 1.078
+  // ms (same box, two rounds), its fp32 twin and CelebA neutral-to-slower at 512
+  static long bf16_tg = -1;
+  if (bf16_tg < 0) {
+    const char* e = getenv("CV_WGRAD_TARGET_BF16");
+    bf16_tg = e ? atol(e) : 512;
+    if (bf16_tg < 0) bf16_tg = 0;
+  }
+  WPlan w = wgrad_plan(a.M, a.N, a.K, split_k, -1, mma == CV_MMA_BF16 ? bf16_tg : 0);
   const int Ntot = a.N + (gbias ? 1 : 0);
   // pixel-major K (a K tile = 32 images at one small pixel; an N tile = one tap): the tile skips the pixels at which
   // its tap reads padding (the split is then re-cut per tile over the pixels it visits)
